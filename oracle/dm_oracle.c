@@ -1,0 +1,283 @@
+/*
+ * dm_oracle.c -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / the timed CPU baseline.  The product path
+ * (deepmatching_stereo_matching_amd/) never links or calls it.
+ *
+ * It follows the reference step by step, deliberately WITHOUT the algebraic shortcuts
+ * the HIP kernels take (pooling before normalisation / rectification, on-demand level-0
+ * recomputation), so that it checks them:
+ *
+ *   dmo_corr_l0    Correlation_map._create_atomic_patch + _create_simple_initial_co_map
+ *                  (misc/Correlation_map.py:51-87) with Feature_value.__call__ / min_max
+ *                  (misc/Feature_value.py:32-43) and the pinned matchTemplate arithmetic
+ *                  of oracle/cv2_shim/cv2.py (OpenCV's own arithmetic is unpinnable).
+ *   dmo_rectify    Correlation_map._rectification  (misc/Correlation_map.py:158-159)
+ *   dmo_aggregate  Correlation_map._aggregation    (misc/Correlation_map.py:89-130),
+ *                  Maxpool = nn.MaxPool2d(3, 2, padding=1) (:176-184), NaN-propagating.
+ *   dmo_match      Matching.__call__ (misc/Matching.py:211-222): _initial_move_map
+ *                  (:80-96), _B / _calc_match (:98-149), _calc_near_match (:58-78),
+ *                  _sub_pix_cal / _sub_pix_compute (:165-209).  (_filter: oracle.py.)
+ *   dmo_cal_map    Calc_difference.cal_map (misc/Calc_difference.py:26-49).
+ *
+ * pow() is the C library's, as numpy's float64 power is in the reference (which itself
+ * may differ by 1 ulp between machines: SVML vs libm, see DESIGN.md "Numerics").
+ *
+ * Parity pinned by the tests/golden npz fixtures, generated from the reference itself.
+ * Build: oracle/Makefile  (gcc -O2 -fopenmp -ffp-contract=off; no fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define DMO_NORMED 5 /* cv2.TM_CCOEFF_NORMED */
+#define DMO_CCOEFF 4 /* cv2.TM_CCOEFF */
+
+/* ---- level 0 -------------------------------------------------------------------- */
+/* img/tmpl: uint8 H x W row-major.  l0: [h0*w0][h0*w0] float32, h0 = H-ws+1. */
+int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
+                int method, float *l0)
+{
+    if (ws < 1 || (ws & 1) == 0 || H < ws || W < ws) return -1;
+    if (method != DMO_NORMED && method != DMO_CCOEFF) return -2;
+    const int h0 = H - ws + 1, w0 = W - ws + 1, n = ws * ws;
+    const long P = (long)h0 * w0;
+    int64_t *sI = malloc(sizeof(int64_t) * P);
+    float *bq = malloc(sizeof(float) * P);
+    for (int q0 = 0; q0 < h0; ++q0)
+        for (int q1 = 0; q1 < w0; ++q1) {
+            int64_t s = 0, s2 = 0;
+            for (int u = 0; u < ws; ++u)
+                for (int v = 0; v < ws; ++v) {
+                    int64_t x = tmpl[(long)(q0 + u) * W + q1 + v];
+                    s += x; s2 += x * x;
+                }
+            long q = (long)q0 * w0 + q1;
+            int64_t dI = (int64_t)n * s2 - s * s;
+            sI[q] = s;
+            bq[q] = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
+        }
+    const float inv_n = (float)(1.0 / n);
+    #pragma omp parallel for schedule(dynamic, 1)
+    for (long p = 0; p < P; ++p) {
+        const int p0 = (int)(p / w0), p1 = (int)(p % w0);
+        int T[15 * 15 + 256];
+        int64_t sT = 0, sT2 = 0;
+        for (int u = 0; u < ws; ++u)
+            for (int v = 0; v < ws; ++v) {
+                int x = img[(long)(p0 + u) * W + p1 + v];
+                T[u * ws + v] = x; sT += x; sT2 += (int64_t)x * x;
+            }
+        float *row = l0 + p * P;
+        const int64_t dT = (int64_t)n * sT2 - sT * sT;
+        const float a = dT == 0 ? 0.0f : (float)(1.0 / sqrt((double)dT));
+        for (int q0 = 0; q0 < h0; ++q0)
+            for (int q1 = 0; q1 < w0; ++q1) {
+                const long q = (long)q0 * w0 + q1;
+                int64_t sTI = 0;
+                for (int u = 0; u < ws; ++u) {
+                    const uint8_t *ir = tmpl + (long)(q0 + u) * W + q1;
+                    for (int v = 0; v < ws; ++v) sTI += (int64_t)T[u * ws + v] * ir[v];
+                }
+                const int64_t num = (int64_t)n * sTI - sT * sI[q];
+                float r;
+                if (method == DMO_CCOEFF) {
+                    r = (float)num * inv_n;
+                } else if (dT == 0) {
+                    r = 1.0f;
+                } else {
+                    const float c = a * bq[q];
+                    r = (float)num * c;
+                    r = r < -1.0f ? -1.0f : (r > 1.0f ? 1.0f : r);
+                }
+                row[q] = r;
+            }
+        /* Feature_value.min_max: (x - min) / (max - min) in float32 */
+        float mn = row[0], mx = row[0];
+        for (long q = 1; q < P; ++q) {
+            if (row[q] < mn) mn = row[q];
+            if (row[q] > mx) mx = row[q];
+        }
+        const float den = mx - mn;
+        for (long q = 0; q < P; ++q) row[q] = (row[q] - mn) / den;
+    }
+    free(sI); free(bq);
+    return 0;
+}
+
+/* ---- rectification: out = (double)in ** lam ------------------------------------- */
+void dmo_rectify_f32(const float *in, long n, double lam, double *out)
+{
+    #pragma omp parallel for schedule(static)
+    for (long i = 0; i < n; ++i) out[i] = pow((double)in[i], lam);
+}
+
+void dmo_rectify_f64(double *inout, long n, double lam)
+{
+    #pragma omp parallel for schedule(static)
+    for (long i = 0; i < n; ++i) inout[i] = pow(inout[i], lam);
+}
+
+/* torch max_pool2d semantics: -inf padding, NaN propagates */
+static inline double nanmax(double acc, double v)
+{
+    return (v > acc || isnan(v)) ? v : acc;
+}
+
+/* ---- aggregation: in (h,w,h,w) f64 -> out (h/2,w/2,h/2,w/2) f64, NOT rectified ----- */
+int dmo_aggregate(const double *in, int h, int w, double *out)
+{
+    if ((h & 1) || (w & 1)) return -1;
+    const int h2 = h / 2, w2 = w / 2;
+    const long P = (long)h * w, P2 = (long)h2 * w2;
+    double *R = malloc(sizeof(double) * P * P2);
+    /* res[i, j] = Maxpool(map[i, j]) for every p */
+    #pragma omp parallel for schedule(static)
+    for (long p = 0; p < P; ++p) {
+        const double *m = in + p * P;
+        double *r = R + p * P2;
+        for (int u = 0; u < h2; ++u)
+            for (int v = 0; v < w2; ++v) {
+                double acc = -INFINITY;
+                for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+                    if (a < 0 || a >= h) continue;
+                    for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                        if (b < 0 || b >= w) continue;
+                        acc = nanmax(acc, m[(long)a * w + b]);
+                    }
+                }
+                r[(long)u * w2 + v] = acc;
+            }
+    }
+    /* output[i, j] = (ul + ur + ll + lr) / 4, left to right */
+    #pragma omp parallel for schedule(static)
+    for (long c = 0; c < P2; ++c) {
+        const int i = (int)(c / w2), j = (int)(c % w2);
+        const double *ul = R + ((long)(2 * i) * w + 2 * j) * P2;
+        const double *ur = R + ((long)(2 * i) * w + 2 * j + 1) * P2;
+        const double *ll = R + ((long)(2 * i + 1) * w + 2 * j) * P2;
+        const double *lr = R + ((long)(2 * i + 1) * w + 2 * j + 1) * P2;
+        double *o = out + c * P2;
+        for (long k = 0; k < P2; ++k) o[k] = (ul[k] + ur[k] + ll[k] + lr[k]) / 4;
+    }
+    free(R);
+    return 0;
+}
+
+/* ---- matching ------------------------------------------------------------------- */
+/* _calc_near_match on map M (h x w) = co_map[p]; returns row, col, score */
+static void near_match(const double *M, int h, int w, int pd0, int pd1, double *o)
+{
+    double win[9];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            const int r = pd0 - 1 + a, c = pd1 - 1 + b;
+            win[a * 3 + b] = (r < 0 || r >= h || c < 0 || c >= w) ? 0.0 : M[(long)r * w + c];
+        }
+    /* np.argmax: first maximum, a NaN wins at its first occurrence; np.max -> NaN */
+    int m = 0, has_nan = isnan(win[0]);
+    double best = win[0];
+    if (!has_nan)
+        for (int k = 1; k < 9; ++k) {
+            if (isnan(win[k])) { m = k; has_nan = 1; break; }
+            if (win[k] > best) { best = win[k]; m = k; }
+        }
+    if (!has_nan && best < 0.0001) m = 4;
+    o[0] = (double)(pd0 + m / 3 - 1);
+    o[1] = (double)(pd1 + m % 3 - 1);
+    o[2] = win[m] + M[(long)pd0 * w + pd1];
+}
+
+static double sub_pix_compute(double r0, double r1, double r_)
+{
+    if (r0 > r1 && r0 > r_) return -(r1 - r_) / (2 * (r1 + r_ - 2 * r0));
+    return 0;
+}
+
+/* levels[l]: (h0>>l, w0>>l, h0>>l, w0>>l) f64 rectified.  out: (3, h0, w0) f64. */
+int dmo_match(const double *const *levels, int nlev, int h0, int w0, int sub_pix,
+              double *out)
+{
+    if (nlev < 2) return -1; /* Matching._B indexes co_map_list[-2] unconditionally */
+    int h = h0 >> (nlev - 1), w = w0 >> (nlev - 1);
+    double *cur = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
+    double *nxt = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
+    const double *L = levels[nlev - 1];
+    long P = (long)h * w;
+    for (int i = 0; i < h; ++i)
+        for (int j = 0; j < w; ++j) {
+            double o[3];
+            near_match(L + ((long)i * w + j) * P, h, w, i, j, o);
+            for (int k = 0; k < 3; ++k) cur[k * P + (long)i * w + j] = o[k];
+        }
+    static const int OFF[4][2] = {{1, 1}, {0, 1}, {1, 0}, {0, 0}};
+    for (int l = nlev - 2; l >= 0; --l) {
+        const int hn = h * 2, wn = w * 2;
+        const long Pn = (long)hn * wn;
+        L = levels[l];
+        for (int i = 0; i < h; ++i)
+            for (int j = 0; j < w; ++j) {
+                const long pc = (long)i * w + j;
+                const int64_t b0 = (int64_t)(cur[pc] * 2), b1 = (int64_t)(cur[P + pc] * 2);
+                for (int k = 0; k < 4; ++k) {
+                    const int p0 = 2 * i + OFF[k][0], p1 = 2 * j + OFF[k][1];
+                    double o[3];
+                    near_match(L + ((long)p0 * wn + p1) * Pn, hn, wn,
+                               (int)(b0 + OFF[k][0]), (int)(b1 + OFF[k][1]), o);
+                    for (int c = 0; c < 3; ++c) nxt[c * Pn + (long)p0 * wn + p1] = o[c];
+                }
+            }
+        double *t = cur; cur = nxt; nxt = t;
+        h = hn; w = wn; P = Pn;
+    }
+    if (sub_pix) {
+        const double *L0 = levels[0];
+        for (int i = 0; i < h0; ++i)
+            for (int j = 0; j < w0; ++j) {
+                const long pc = (long)i * w0 + j;
+                const double *M = L0 + pc * P;
+                const int c0 = (int)cur[pc], c1 = (int)cur[P + pc];
+                const double d_x = i - cur[pc];
+                if (c0 + 1 >= h0) {
+                    cur[pc] = i - d_x;                       /* IndexError branch */
+                } else {
+                    const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1; /* python wraps -1 */
+                    const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)(c0 + 1) * w0 + c1],
+                                 r_ = M[(long)cm * w0 + c1];
+                    cur[pc] = i - d_x + sub_pix_compute(r0, r1, r_);
+                }
+                const double d_y = j - cur[P + pc];
+                if (c1 + 1 >= w0) {
+                    cur[P + pc] = j - d_y;
+                } else {
+                    const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
+                    const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)c0 * w0 + c1 + 1],
+                                 r_ = M[(long)c0 * w0 + cm];
+                    cur[P + pc] = j - d_y + sub_pix_compute(r0, r1, r_);
+                }
+            }
+    }
+    memcpy(out, cur, sizeof(double) * 3 * P);
+    free(cur); free(nxt);
+    return 0;
+}
+
+/* mode: 0 elevation (j - map[1]), 1 elevation2 (i - map[0]), 2 distance */
+int dmo_cal_map(const double *map, int h, int w, int mode, double *out)
+{
+    const long P = (long)h * w;
+    if (mode < 0 || mode > 2) return -1;
+    for (int i = 0; i < h; ++i)
+        for (int j = 0; j < w; ++j) {
+            const long k = (long)i * w + j;
+            if (mode == 0) out[k] = (double)j - map[P + k];
+            else if (mode == 1) out[k] = (double)i - map[k];
+            else {
+                const double a = (double)i - map[k], b = (double)j - map[P + k];
+                out[k] = sqrt(a * a + b * b);
+            }
+        }
+    return 0;
+}
