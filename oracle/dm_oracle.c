@@ -32,6 +32,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../deepmatching_stereo_matching_amd/csrc/dm_pow.h"
+
 #define DMO_NORMED 5 /* cv2.TM_CCOEFF_NORMED */
 #define DMO_CCOEFF 4 /* cv2.TM_CCOEFF */
 
@@ -40,7 +42,7 @@
 int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
                 int method, float *l0)
 {
-    if (ws < 1 || (ws & 1) == 0 || H < ws || W < ws) return -1;
+    if (ws < 1 || (ws & 1) == 0 || H < ws || W < ws || ws > 21) return -1;
     if (method != DMO_NORMED && method != DMO_CCOEFF) return -2;
     const int h0 = H - ws + 1, w0 = W - ws + 1, n = ws * ws;
     const long P = (long)h0 * w0;
@@ -108,16 +110,32 @@ int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
 }
 
 /* ---- rectification: out = (double)in ** lam ------------------------------------- */
+/* pow mode 0: the C library's pow (as numpy on this host); mode 1: the build's pinned
+ * dm_pow14 (dm_pow.h), which the GPU kernels use -- GPU parity tests select it so that
+ * every float64 output can be compared bit for bit. */
+static int g_pow_mode = 0;
+static const double POW_TAB[] = DM_POW_TAB_INIT;
+static const double POW_G[] = DM_POW_G_INIT;
+
+void dmo_set_pow_mode(int mode) { g_pow_mode = mode; }
+
+double dmo_pow14(double x) { return dm_pow14(x, POW_TAB, POW_G); }
+
+static inline double rect(double x, double lam)
+{
+    return g_pow_mode == 1 ? dm_pow14(x, POW_TAB, POW_G) : pow(x, lam);
+}
+
 void dmo_rectify_f32(const float *in, long n, double lam, double *out)
 {
     #pragma omp parallel for schedule(static)
-    for (long i = 0; i < n; ++i) out[i] = pow((double)in[i], lam);
+    for (long i = 0; i < n; ++i) out[i] = rect((double)in[i], lam);
 }
 
 void dmo_rectify_f64(double *inout, long n, double lam)
 {
     #pragma omp parallel for schedule(static)
-    for (long i = 0; i < n; ++i) inout[i] = pow(inout[i], lam);
+    for (long i = 0; i < n; ++i) inout[i] = rect(inout[i], lam);
 }
 
 /* torch max_pool2d semantics: -inf padding, NaN propagates */

@@ -46,8 +46,20 @@ def lib():
         L.dmo_aggregate.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
         L.dmo_match.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.dmo_cal_map.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        L.dmo_set_pow_mode.argtypes = [ctypes.c_int]
+        L.dmo_pow14.argtypes = [ctypes.c_double]
+        L.dmo_pow14.restype = ctypes.c_double
         _lib = L
     return _lib
+
+
+def set_pow_mode(mode):
+    """'libm' (numpy-like, default) or 'pinned' (dm_pow.h, what the GPU computes)."""
+    lib().dmo_set_pow_mode({'libm': 0, 'pinned': 1}[mode])
+
+
+def pow14(x):
+    return lib().dmo_pow14(float(x))
 
 
 def _p(a):

@@ -36,8 +36,17 @@ def _close(a, b, tol):
         assert np.max(np.abs(a[~na] - b[~na])) <= tol
 
 
+@pytest.fixture(scope='module', params=['libm', 'pinned'])
+def pow_mode(request):
+    """Both rectification pows must reproduce the reference: libm (numpy's, here) and the
+    build's pinned dm_pow14 that the GPU kernels evaluate."""
+    O.set_pow_mode(request.param)
+    yield request.param
+    O.set_pow_mode('libm')
+
+
 @pytest.fixture(scope='module', params=PAIRS, ids=lambda p: os.path.basename(p)[:-4])
-def case(request):
+def case(request, pow_mode):
     g = dict(np.load(request.param))
     l0 = O.corr_l0(g['img1'], g['img2'], int(g['ws']), str(g['feature']))
     levels, it, n_map = O.pyramid(l0)
