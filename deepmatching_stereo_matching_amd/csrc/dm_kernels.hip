@@ -1,0 +1,816 @@
+// dm_kernels.hip -- gfx950 kernels + C ABI (include/dmstereo.h) of the DeepMatching stereo
+// correlation engine.  Reference: Yuki-Kumon/deepmatching_stereo_matching, misc/*.py.
+//
+// Numerics (DESIGN.md "Numerics"): the level-0 value of patch p against window q is
+//   num = n*sum(T'I') - sum(T')*sum(I')      exact int32 (T' = T-128, I' = I-128; shift-free)
+//   y   = f32(num) * b_q                      b_q = f32(1/sqrt(dI)) (0 if dI == 0) | 1 (CCOEFF)
+//   r   = clamp(y * a_p, -1, 1)               a_p = f32(1/sqrt(dT)) | f32(1/n) (CCOEFF, no clamp)
+//   x   = (r - rmin_p) / (rmax_p - rmin_p)    float32, Feature_value.min_max
+//   L0  = pow14(x)                            float64, Correlation_map._rectification
+// y -> r -> x -> pow14 is monotone non-decreasing for a fixed p, so MaxPool and min/max are
+// taken on y and only pooled values are normalised and rectified.  All float ops are
+// explicit-rounding (__fmul_rn etc.); the file is compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/dmstereo.h"
+#include "dm_pow.h"
+
+__constant__ double c_pow_tab[DM_POW_NT * 3] = DM_POW_TAB_INIT;
+__constant__ double c_pow_g[10] = DM_POW_G_INIT;
+
+__device__ __forceinline__ double pow14(double x) { return dm_pow14(x, c_pow_tab, c_pow_g); }
+
+// ------------------------------------------------------------------------------------
+// geometry + workspace views
+// ------------------------------------------------------------------------------------
+struct Geo {
+    const uint8_t *img1, *img2;
+    int pitch1, pitch2;
+    const int *org;
+    int T, h0, w0, ws, method;
+};
+
+struct Stats {
+    int *sT;    // sum(T') per patch         [T][P]
+    float *aP;  // a_p                        [T][P]
+    int *sI;    // sum(I') per window         [T][P]
+    float *bQ;  // b_q                        [T][P]
+    float *rmn; // min_q r(p, q)              [T][P]
+    float *rmx; // max_q r(p, q)              [T][P]
+};
+
+static Stats stats_view(void *base, int T, int P)
+{
+    Stats s;
+    char *c = (char *)base;
+    const size_t n = (size_t)T * P;
+    s.sT = (int *)c;
+    s.aP = (float *)(c + 4 * n);
+    s.sI = (int *)(c + 8 * n);
+    s.bQ = (float *)(c + 12 * n);
+    s.rmn = (float *)(c + 16 * n);
+    s.rmx = (float *)(c + 20 * n);
+    return s;
+}
+
+__device__ __forceinline__ float r_of_y(float y, float a, int method)
+{
+    if (method == DM_TM_CCOEFF) return __fmul_rn(y, a);
+    if (a == 0.0f) return 1.0f; // constant patch: OpenCV returns 1 everywhere
+    const float r = __fmul_rn(y, a);
+    return r < -1.0f ? -1.0f : (r > 1.0f ? 1.0f : r);
+}
+
+__device__ __forceinline__ float y_of_num(int num, float b) { return __fmul_rn((float)num, b); }
+
+__device__ __forceinline__ float norm_x(float r, float mn, float mx)
+{
+    return __fdiv_rn(__fsub_rn(r, mn), __fsub_rn(mx, mn));
+}
+
+// ------------------------------------------------------------------------------------
+// K1: per-patch / per-window moments
+// ------------------------------------------------------------------------------------
+__global__ void k_stats(Geo g, Stats s)
+{
+    const int P = g.h0 * g.w0;
+    const int t = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int p0 = p / g.w0, p1 = p % g.w0;
+    const int r0 = g.org[2 * t] + p0, c0 = g.org[2 * t + 1] + p1;
+    const int n = g.ws * g.ws;
+    int sa = 0, sa2 = 0, sb = 0, sb2 = 0;
+    for (int u = 0; u < g.ws; ++u)
+        for (int v = 0; v < g.ws; ++v) {
+            const int a = (int)g.img1[(size_t)(r0 + u) * g.pitch1 + c0 + v] - 128;
+            const int b = (int)g.img2[(size_t)(r0 + u) * g.pitch2 + c0 + v] - 128;
+            sa += a; sa2 += a * a; sb += b; sb2 += b * b;
+        }
+    const long long dT = (long long)n * sa2 - (long long)sa * sa;
+    const long long dI = (long long)n * sb2 - (long long)sb * sb;
+    float ap, bq;
+    if (g.method == DM_TM_CCOEFF) {
+        ap = (float)(1.0 / (double)n);
+        bq = 1.0f;
+    } else {
+        ap = dT == 0 ? 0.0f : (float)(1.0 / sqrt((double)dT));
+        bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
+    }
+    const size_t o = (size_t)t * P + p;
+    s.sT[o] = sa; s.aP[o] = ap; s.sI[o] = sb; s.bQ[o] = bq;
+}
+
+// exact numerator for (patch p0,p1 ; window q0,q1) of tile t, read from global images
+__device__ int num_global(const Geo &g, int t, int p0, int p1, int q0, int q1, int sT, int sI)
+{
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+    int acc = 0;
+    for (int u = 0; u < g.ws; ++u) {
+        const uint8_t *a = g.img1 + (size_t)(ro + p0 + u) * g.pitch1 + co + p1;
+        const uint8_t *b = g.img2 + (size_t)(ro + q0 + u) * g.pitch2 + co + q1;
+        for (int v = 0; v < g.ws; ++v) acc += ((int)a[v] - 128) * ((int)b[v] - 128);
+    }
+    return g.ws * g.ws * acc - sT * sI;
+}
+
+// rectified level-0 value L0[p][q] (co_map_list[0]), evaluated on demand
+__device__ double l0_value(const Geo &g, const Stats &s, int t, int p0, int p1, int q0, int q1)
+{
+    const int P = g.h0 * g.w0;
+    const size_t op = (size_t)t * P + p0 * g.w0 + p1, oq = (size_t)t * P + q0 * g.w0 + q1;
+    const int num = num_global(g, t, p0, p1, q0, q1, s.sT[op], s.sI[oq]);
+    const float r = r_of_y(y_of_num(num, s.bQ[oq]), s.aP[op], g.method);
+    return pow14((double)norm_x(r, s.rmn[op], s.rmx[op]));
+}
+
+// ------------------------------------------------------------------------------------
+// K2 (generic): one workgroup per level-1 cell (= 2x2 block of patches p).  For each
+// child p in reference order ul, ur, ll, lr: y over all windows q -> LDS, block min/max,
+// MaxPool(3,2,1) on y, normalise + rectify the pooled values, accumulate the children
+// in order; finally /4 and rectify -> level 1.  Requires P <= DM_GENERIC_MAX_P.
+// ------------------------------------------------------------------------------------
+#define DM_GENERIC_MAX_P 16384
+#define K2_THREADS 256
+
+template <int WS>
+__global__ __launch_bounds__(K2_THREADS) void k_level1_generic(Geo g, Stats s, double *L1)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int h0 = g.h0, w0 = g.w0, P = h0 * w0;
+    const int h1 = h0 / 2, w1 = w0 / 2, P1 = h1 * w1;
+    const int t = blockIdx.y, cell = blockIdx.x;
+    const int I = cell / w1, J = cell % w1;
+    const int Wc = w0 + WS - 1, Hc = h0 + WS - 1;
+    const int tid = threadIdx.x;
+    float *ymap = (float *)smem;                                   // [P]
+    double *acc = (double *)(smem + (size_t)P * 4);                // [P1]
+    float *red = (float *)(smem + (size_t)P * 4 + (size_t)P1 * 8); // [2*K2_THREADS/64]
+    signed char *crop = (signed char *)(red + 2 * (K2_THREADS / 64));
+    signed char *patch = crop + Hc * Wc;                           // [WS*WS]
+
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+    for (int i = tid; i < Hc * Wc; i += K2_THREADS) {
+        const int r = i / Wc, c = i % Wc;
+        crop[i] = (signed char)((int)g.img2[(size_t)(ro + r) * g.pitch2 + co + c] - 128);
+    }
+    const size_t tb = (size_t)t * P;
+    const int n = WS * WS;
+    for (int ch = 0; ch < 4; ++ch) {
+        const int p0 = 2 * I + (ch >> 1), p1 = 2 * J + (ch & 1);
+        const int p = p0 * w0 + p1;
+        __syncthreads(); // previous child done with patch / ymap / red
+        if (tid < n) {
+            const int u = tid / WS, v = tid % WS;
+            patch[tid] = (signed char)((int)g.img1[(size_t)(ro + p0 + u) * g.pitch1 + co + p1 + v] - 128);
+        }
+        __syncthreads();
+        int Tr[WS * WS];
+#pragma unroll
+        for (int k = 0; k < WS * WS; ++k) Tr[k] = patch[k];
+        const int sT = s.sT[tb + p];
+        const float ap = s.aP[tb + p];
+        float ymn = INFINITY, ymx = -INFINITY;
+        for (int q = tid; q < P; q += K2_THREADS) {
+            const int q0 = q / w0, q1 = q % w0;
+            int a = 0;
+#pragma unroll
+            for (int u = 0; u < WS; ++u)
+#pragma unroll
+                for (int v = 0; v < WS; ++v) a += Tr[u * WS + v] * (int)crop[(q0 + u) * Wc + q1 + v];
+            const float y = y_of_num(n * a - sT * s.sI[tb + q], s.bQ[tb + q]);
+            ymap[q] = y;
+            ymn = fminf(ymn, y);
+            ymx = fmaxf(ymx, y);
+        }
+        // block min / max
+        for (int off = 32; off > 0; off >>= 1) {
+            ymn = fminf(ymn, __shfl_xor(ymn, off));
+            ymx = fmaxf(ymx, __shfl_xor(ymx, off));
+        }
+        if ((tid & 63) == 0) { red[tid >> 6] = ymn; red[K2_THREADS / 64 + (tid >> 6)] = ymx; }
+        __syncthreads();
+        ymn = red[0]; ymx = red[K2_THREADS / 64];
+        for (int k = 1; k < K2_THREADS / 64; ++k) {
+            ymn = fminf(ymn, red[k]);
+            ymx = fmaxf(ymx, red[K2_THREADS / 64 + k]);
+        }
+        const float rmn = r_of_y(ymn, ap, g.method), rmx = r_of_y(ymx, ap, g.method);
+        if (tid == 0) { s.rmn[tb + p] = rmn; s.rmx[tb + p] = rmx; }
+        // pooled, normalised, rectified child accumulated in reference order
+        for (int k = tid; k < P1; k += K2_THREADS) {
+            const int u = k / w1, v = k % w1;
+            float m = -INFINITY;
+            for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+                if (a < 0 || a >= h0) continue;
+                for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                    if (b < 0 || b >= w0) continue;
+                    m = fmaxf(m, ymap[a * w0 + b]);
+                }
+            }
+            const double val = pow14((double)norm_x(r_of_y(m, ap, g.method), rmn, rmx));
+            acc[k] = ch == 0 ? val : acc[k] + val;
+        }
+    }
+    __syncthreads();
+    double *out = L1 + ((size_t)t * P1 + cell) * P1;
+    for (int k = tid; k < P1; k += K2_THREADS) out[k] = pow14(acc[k] / 4.0);
+}
+
+static size_t k2_lds_bytes(int h0, int w0, int ws)
+{
+    const size_t P = (size_t)h0 * w0, P1 = P / 4;
+    return P * 4 + P1 * 8 + 2 * (K2_THREADS / 64) * 4 + (size_t)(h0 + ws - 1) * (w0 + ws - 1) + ws * ws;
+}
+
+// ------------------------------------------------------------------------------------
+// level-0 volume (co_map) materialisation: pass 1 min/max, pass 2 coalesced f32 stores
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_minmax(Geo g, Stats s)
+{
+    const int P = g.h0 * g.w0, t = blockIdx.y, p = blockIdx.x;
+    const int p0 = p / g.w0, p1 = p % g.w0;
+    const size_t tb = (size_t)t * P;
+    const int sT = s.sT[tb + p];
+    const float ap = s.aP[tb + p];
+    float ymn = INFINITY, ymx = -INFINITY;
+    for (int q = threadIdx.x; q < P; q += 256) {
+        const float y = y_of_num(num_global(g, t, p0, p1, q / g.w0, q % g.w0, sT, s.sI[tb + q]), s.bQ[tb + q]);
+        ymn = fminf(ymn, y);
+        ymx = fmaxf(ymx, y);
+    }
+    __shared__ float red[8];
+    for (int off = 32; off > 0; off >>= 1) {
+        ymn = fminf(ymn, __shfl_xor(ymn, off));
+        ymx = fmaxf(ymx, __shfl_xor(ymx, off));
+    }
+    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = ymn; red[4 + (threadIdx.x >> 6)] = ymx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ymn = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+        ymx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+        s.rmn[tb + p] = r_of_y(ymn, ap, g.method);
+        s.rmx[tb + p] = r_of_y(ymx, ap, g.method);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_volume(Geo g, Stats s, float *l0)
+{
+    const int P = g.h0 * g.w0, t = blockIdx.y, p = blockIdx.x;
+    const int p0 = p / g.w0, p1 = p % g.w0;
+    const size_t tb = (size_t)t * P;
+    const int sT = s.sT[tb + p];
+    const float ap = s.aP[tb + p], mn = s.rmn[tb + p], mx = s.rmx[tb + p];
+    float *row = l0 + (tb + p) * P;
+    for (int q = threadIdx.x; q < P; q += 256) {
+        const float y = y_of_num(num_global(g, t, p0, p1, q / g.w0, q % g.w0, sT, s.sI[tb + q]), s.bQ[tb + q]);
+        row[q] = norm_x(r_of_y(y, ap, g.method), mn, mx);
+    }
+}
+
+template <typename F>
+__global__ void k_rectify(const F *in, size_t n, double *out)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = pow14((double)in[i]);
+}
+
+// ------------------------------------------------------------------------------------
+// pyramid step for levels >= 1 (float64 in, float64 out)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ double nanmax(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
+
+__global__ void k_aggregate(const double *in, int T, int h, int w, int rectify, double *out)
+{
+    const int h2 = h / 2, w2 = w / 2;
+    const size_t P = (size_t)h * w, P2 = (size_t)h2 * w2;
+    const size_t total = (size_t)T * P2 * P2;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t t = idx / (P2 * P2);
+        const size_t rem = idx % (P2 * P2);
+        const int cell = (int)(rem / P2), k = (int)(rem % P2);
+        const int I = cell / w2, J = cell % w2, u = k / w2, v = k % w2;
+        double acc = 0.0;
+        for (int ch = 0; ch < 4; ++ch) {
+            const int c = (2 * I + (ch >> 1)) * w + 2 * J + (ch & 1);
+            const double *m = in + (t * P + c) * P;
+            double mx = -INFINITY;
+            for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+                if (a < 0 || a >= h) continue;
+                for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                    if (b < 0 || b >= w) continue;
+                    mx = nanmax(mx, m[(size_t)a * w + b]);
+                }
+            }
+            acc = ch == 0 ? mx : acc + mx;
+        }
+        out[idx] = rectify ? pow14(acc / 4.0) : acc / 4.0;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// matching (Matching.py)
+// ------------------------------------------------------------------------------------
+struct Levels {
+    const double *lv[32];
+};
+
+// Matching._calc_near_match (:58-78) on a 3x3 zero-padded window of values win[9]
+__device__ __forceinline__ void near_pick(const double *win, int pd0, int pd1, double *o)
+{
+    int m = 0;
+    bool nan_seen = isnan(win[0]);
+    double best = win[0];
+    if (!nan_seen) {
+        for (int k = 1; k < 9; ++k) {
+            if (isnan(win[k])) { m = k; nan_seen = true; break; }
+            if (win[k] > best) { best = win[k]; m = k; }
+        }
+    }
+    if (!nan_seen && best < 0.0001) m = 4;
+    o[0] = (double)(pd0 + m / 3 - 1);
+    o[1] = (double)(pd1 + m % 3 - 1);
+    o[2] = win[m] + win[4];
+}
+
+__device__ __forceinline__ void window_lvl(const double *M, int h, int w, int pd0, int pd1, double *win)
+{
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            const int r = pd0 - 1 + a, c = pd1 - 1 + b;
+            win[a * 3 + b] = (r < 0 || r >= h || c < 0 || c >= w) ? 0.0 : M[(size_t)r * w + c];
+        }
+}
+
+// top of the pyramid (_initial_move_map, :80-96): p_dot = p
+__global__ void k_match_top(const double *LK, int T, int h, int w, double *map)
+{
+    const size_t P = (size_t)h * w;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    const size_t t = idx / P, p = idx % P;
+    const int i = (int)(p / w), j = (int)(p % w);
+    double win[9], o[3];
+    window_lvl(LK + (t * P + p) * P, h, w, i, j, win);
+    near_pick(win, i, j, o);
+    double *mt = map + t * 3 * P;
+    mt[p] = o[0]; mt[P + p] = o[1]; mt[2 * P + p] = o[2];
+}
+
+__device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r_)
+{
+    if (r0 > r1 && r0 > r_) return -(r1 - r_) / (2.0 * (r1 + r_ - 2.0 * r0));
+    return 0.0;
+}
+
+// one _B step (:98-139): parent map (h x w) -> child map (2h x 2w) on level L (materialised
+// when L != nullptr, else level 0 on demand); at level 0 optionally _sub_pix_cal (:177-209)
+__global__ void k_match_step(Geo g, Stats s, const double *L, int T, int h, int w,
+                             const double *pmap, double *cmap)
+{
+    const int hn = 2 * h, wn = 2 * w;
+    const size_t P = (size_t)h * w, Pn = (size_t)hn * wn;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * Pn) return;
+    const int t = (int)(idx / Pn);
+    const int pc = (int)(idx % Pn);
+    const int p0 = pc / wn, p1 = pc % wn;
+    const int o0 = p0 & 1, o1 = p1 & 1;
+    const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
+    const double *pm = pmap + (size_t)t * 3 * P;
+    const int pd0 = (int)(long long)(pm[par] * 2) + o0;
+    const int pd1 = (int)(long long)(pm[P + par] * 2) + o1;
+    double win[9], o[3];
+    if (L) {
+        window_lvl(L + ((size_t)t * Pn + pc) * Pn, hn, wn, pd0, pd1, win);
+    } else {
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                const int r = pd0 - 1 + a, c = pd1 - 1 + b;
+                win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0 : l0_value(g, s, t, p0, p1, r, c);
+            }
+    }
+    near_pick(win, pd0, pd1, o);
+    double *cm_ = cmap + (size_t)t * 3 * Pn;
+    cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
+}
+
+// Matching._sub_pix_cal (:177-209) on the final level-0 map, in place.  L0: materialised
+// rectified level 0 ([T][P][P]) or nullptr (on demand from images + stats).
+__global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, double *map)
+{
+    const size_t P = (size_t)h0 * w0;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    const int t = (int)(idx / P), pc = (int)(idx % P);
+    const int p0 = pc / w0, p1 = pc % w0;
+    double *mt = map + (size_t)t * 3 * P;
+    const double *M = L0 ? L0 + ((size_t)t * P + pc) * P : nullptr;
+#define L0V(r_, c_) (M ? M[(size_t)(r_) * w0 + (c_)] : l0_value(g, s, t, p0, p1, (r_), (c_)))
+    const double row = mt[pc], col = mt[P + pc];
+    const int c0 = (int)row, c1 = (int)col; // int() truncation of exact integers
+    const double r0 = L0V(c0, c1);
+    const double dx = (double)p0 - row;
+    double nrow, ncol;
+    if (c0 + 1 >= h0) {
+        nrow = (double)p0 - dx; // IndexError branch (:196-197)
+    } else {
+        const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1; // python index -1 wraps
+        nrow = ((double)p0 - dx) + sub_pix_compute(r0, L0V(c0 + 1, c1), L0V(cm, c1));
+    }
+    const double dy = (double)p1 - col;
+    if (c1 + 1 >= w0) {
+        ncol = (double)p1 - dy;
+    } else {
+        const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
+        ncol = ((double)p1 - dy) + sub_pix_compute(r0, L0V(c0, c1 + 1), L0V(c0, cm));
+    }
+#undef L0V
+    mt[pc] = nrow;
+    mt[P + pc] = ncol;
+}
+
+// Matching._filter (:224-255), square maps: per interior pixel the rounded (half-even)
+// mean / median of the neighbouring integer displacements.  in -> out (score copied).
+__global__ void k_filter(const double *in, double *out, int T, int h, int w, int fw, int median)
+{
+    const size_t P = (size_t)h * w;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    const int t = (int)(idx / P), k = (int)(idx % P);
+    const int i = k / w, j = k % w;
+    const double *mi = in + (size_t)t * 3 * P;
+    double *mo = out + (size_t)t * 3 * P;
+    const int ex = (fw - 1) / 2;
+    double r0 = mi[k], r1 = mi[P + k];
+    if (i >= ex && i < h - ex && j >= ex && j < w - ex) {
+        long long d1[49], d2[49];
+        int n = 0;
+        for (int a = i - ex; a <= i + ex; ++a)
+            for (int b = j - ex; b <= j + ex; ++b) {
+                d1[n] = (long long)mi[P + (size_t)a * w + b] - b; // d_map  = map[1] - j
+                d2[n] = (long long)mi[(size_t)a * w + b] - a;     // d_map2 = map[0] - i
+                ++n;
+            }
+        double v1, v2;
+        if (median) {
+            for (int x = 1; x < n; ++x) // insertion sort, n <= 49
+                for (int y = x; y > 0 && d1[y - 1] > d1[y]; --y) { long long q = d1[y]; d1[y] = d1[y - 1]; d1[y - 1] = q; }
+            for (int x = 1; x < n; ++x)
+                for (int y = x; y > 0 && d2[y - 1] > d2[y]; --y) { long long q = d2[y]; d2[y] = d2[y - 1]; d2[y - 1] = q; }
+            v1 = (double)d1[n / 2];
+            v2 = (double)d2[n / 2];
+        } else {
+            long long s1 = 0, s2 = 0;
+            for (int x = 0; x < n; ++x) { s1 += d1[x]; s2 += d2[x]; }
+            v1 = (double)s1 / (double)n;
+            v2 = (double)s2 / (double)n;
+        }
+        r1 = rint(v1) + (double)j; // python round(): half to even
+        r0 = rint(v2) + (double)i;
+    }
+    mo[k] = r0;
+    mo[P + k] = r1;
+    mo[2 * P + k] = mi[2 * P + k];
+}
+
+__global__ void k_cal_map(const double *map, int T, int h, int w, int mode, double *out)
+{
+    const size_t P = (size_t)h * w;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    const size_t t = idx / P, k = idx % P;
+    const int i = (int)(k / w), j = (int)(k % w);
+    const double *m = map + t * 3 * P;
+    double v;
+    if (mode == DM_CAL_ELEVATION) v = (double)j - m[P + k];
+    else if (mode == DM_CAL_ELEVATION2) v = (double)i - m[k];
+    else {
+        const double a = (double)i - m[k], b = (double)j - m[P + k];
+        v = sqrt(a * a + b * b);
+    }
+    out[idx] = v;
+}
+
+// misc/sub_pix_cal.py:22-53 (image_threshold: misc/optimize_loop.py:40-44)
+__device__ __forceinline__ double thr3(double v) { v = v > 3.0 ? 3.0 : v; return v < -3.0 ? -3.0 : v; }
+
+__global__ void k_sub_pix_cal(const double *arr, const double *co, int h, int w, int dir, double ratio,
+                              double *out)
+{
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)h * w) return;
+    const int i = (int)(idx / w), j = (int)(idx % w);
+    const double d = thr3(arr[idx]);
+    double dis = d;
+    if (i >= 1 && i < h - 1 && j >= 1 && j < w - 1) {
+        const size_t pl = dir == 0 ? idx + w : idx + 1, mi = dir == 0 ? idx - w : idx - 1;
+        const double r0 = co[idx] * ratio, r1 = co[pl] * ratio, r_ = co[mi] * ratio;
+        dis = d - (r1 - r_) / (2.0 * (r1 + r_ - 2.0 * r0));
+        if (fabs(d - dis) > 1.0) dis = d;
+    }
+    out[idx] = thr3(dis);
+}
+
+struct Modes {
+    int m[8];
+};
+
+__global__ void k_stitch(const double *match, int n0, int n1, int h0, int w0, int s0, int s1,
+                         Modes modes, int nmodes, double *dmap, double *score, int Hout, int Wout)
+{
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)Hout * Wout) return;
+    const int y = (int)(idx / Wout), x = (int)(idx % Wout);
+    const int i = min(y / s0, n0 - 1), j = min(x / s1, n1 - 1);
+    const int ly = y - i * s0, lx = x - j * s1;
+    const size_t HW = (size_t)Hout * Wout;
+    if (ly >= h0 || lx >= w0) {
+        for (int k = 0; k < nmodes; ++k) dmap[k * HW + idx] = NAN;
+        score[idx] = NAN;
+        return;
+    }
+    const size_t P = (size_t)h0 * w0, l = (size_t)ly * w0 + lx;
+    const double *m = match + (size_t)(j * n0 + i) * 3 * P;
+    for (int k = 0; k < nmodes; ++k) {
+        double v;
+        if (modes.m[k] == DM_CAL_ELEVATION) v = (double)lx - m[P + l];
+        else if (modes.m[k] == DM_CAL_ELEVATION2) v = (double)ly - m[l];
+        else {
+            const double a = (double)ly - m[l], b = (double)lx - m[P + l];
+            v = sqrt(a * a + b * b);
+        }
+        dmap[k * HW + idx] = v;
+    }
+    score[idx] = m[2 * P + l];
+}
+
+// ------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------
+static thread_local char g_err[512];
+
+static int fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(x)                                                                          \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) return fail(DM_ERR_HIP, "HIP error: %s (%d)", hipGetErrorString(e_), (int)e_); \
+    } while (0)
+
+static int check_tiles(const dm_tiles *b)
+{
+    if (!b || !b->d_img1 || !b->d_img2 || !b->d_origins) return fail(DM_ERR_ARG, "null tile batch / pointer");
+    if (b->T < 1 || b->h0 < 1 || b->w0 < 1) return fail(DM_ERR_ARG, "empty batch (T=%d, h0=%d, w0=%d)", b->T, b->h0, b->w0);
+    if (b->ws < 1 || (b->ws & 1) == 0)
+        return fail(DM_ERR_SHAPE, "window_size must be odd (got %d): Correlation_map.py:63-64 broadcast error", b->ws);
+    if (b->ws > 15) return fail(DM_ERR_UNSUPPORTED, "window_size %d > 15 not supported", b->ws);
+    if (b->method != DM_TM_CCOEFF && b->method != DM_TM_CCOEFF_NORMED)
+        return fail(DM_ERR_ARG, "invalid feature method %d", b->method);
+    return DM_OK;
+}
+
+static Geo make_geo(const dm_tiles *b)
+{
+    Geo g;
+    g.img1 = b->d_img1; g.img2 = b->d_img2;
+    g.pitch1 = b->pitch1; g.pitch2 = b->pitch2;
+    g.org = b->d_origins;
+    g.T = b->T; g.h0 = b->h0; g.w0 = b->w0; g.ws = b->ws; g.method = b->method;
+    return g;
+}
+
+static inline unsigned nblk(size_t n, unsigned bs)
+{
+    size_t b = (n + bs - 1) / bs;
+    return (unsigned)(b > 0x7fffffff ? 0x7fffffff : b);
+}
+
+template <int WS>
+static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
+{
+    const size_t lds = k2_lds_bytes(b->h0, b->w0, WS);
+    static bool attr_set = false; // idempotent attribute, benign race
+    if (!attr_set) {
+        HIP_TRY(hipFuncSetAttribute((const void *)k_level1_generic<WS>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    dim3 grid((b->h0 / 2) * (b->w0 / 2), b->T);
+    k_level1_generic<WS><<<grid, K2_THREADS, lds, st>>>(make_geo(b), s, L1);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+extern "C" {
+
+int dm_abi_version(void) { return 100; }
+
+const char *dm_last_error(void) { return g_err; }
+
+size_t dm_stats_bytes(const dm_tiles *b)
+{
+    if (!b) return 0;
+    return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0;
+}
+
+int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats) return fail(DM_ERR_ARG, "null stats workspace");
+    const int P = b->h0 * b->w0;
+    dim3 grid(nblk(P, 256), b->T);
+    k_stats<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), stats_view(d_stats, b->T, P));
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats || !d_level1) return fail(DM_ERR_ARG, "null workspace / output");
+    if ((b->h0 & 1) || (b->w0 & 1))
+        return fail(DM_ERR_SHAPE, "could not broadcast: map sides %dx%d must be even (Correlation_map.py:96-103)", b->h0, b->w0);
+    const int P = b->h0 * b->w0;
+    if (P > DM_GENERIC_MAX_P || k2_lds_bytes(b->h0, b->w0, b->ws) > 160 * 1024)
+        return fail(DM_ERR_UNSUPPORTED, "tile too large for the generic level-1 kernel (P=%d)", P);
+    Stats s = stats_view(d_stats, b->T, P);
+    hipStream_t st = (hipStream_t)stream;
+    switch (b->ws) {
+    case 1: return launch_level1<1>(b, s, d_level1, st);
+    case 3: return launch_level1<3>(b, s, d_level1, st);
+    case 5: return launch_level1<5>(b, s, d_level1, st);
+    case 7: return launch_level1<7>(b, s, d_level1, st);
+    case 9: return launch_level1<9>(b, s, d_level1, st);
+    case 11: return launch_level1<11>(b, s, d_level1, st);
+    case 13: return launch_level1<13>(b, s, d_level1, st);
+    case 15: return launch_level1<15>(b, s, d_level1, st);
+    }
+    return fail(DM_ERR_UNSUPPORTED, "window size %d", b->ws);
+}
+
+int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats || !d_l0) return fail(DM_ERR_ARG, "null workspace / output");
+    const int P = b->h0 * b->w0;
+    Stats s = stats_view(d_stats, b->T, P);
+    dim3 grid(P, b->T);
+    k_minmax<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s);
+    HIP_TRY(hipGetLastError());
+    k_volume<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s, d_l0);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_rectify(const float *d_in, size_t n, double *d_out, void *stream)
+{
+    if (!d_in || !d_out) return fail(DM_ERR_ARG, "null pointer");
+    if (n == 0) return DM_OK;
+    k_rectify<float><<<nblk(n, 256) > 8192 ? 8192 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_in, n, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_rectify64(const double *d_in, size_t n, double *d_out, void *stream)
+{
+    if (!d_in || !d_out) return fail(DM_ERR_ARG, "null pointer");
+    if (n == 0) return DM_OK;
+    k_rectify<double><<<nblk(n, 256) > 8192 ? 8192 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_in, n, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t rectify, double *d_out,
+                 void *stream)
+{
+    if (!d_in || !d_out || T < 1 || h < 1 || w < 1) return fail(DM_ERR_ARG, "bad aggregate arguments");
+    if ((h & 1) || (w & 1))
+        return fail(DM_ERR_SHAPE, "could not broadcast: map side %d must halve (Correlation_map.py:96-103)", (h & 1) ? h : w);
+    const size_t n = (size_t)T * (h / 2) * (w / 2) * (h / 2) * (w / 2);
+    k_aggregate<<<nblk(n, 256) > 65536 ? 65536 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_in, T, h, w, rectify, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_levels, int32_t nlev,
+             int32_t T, int32_t h0, int32_t w0, int32_t sub_pix, int32_t filter_window,
+             int32_t filter_num, int32_t filter_mode, double *d_scratch, double *d_out, void *stream)
+{
+    if (!d_levels || !d_scratch || !d_out) return fail(DM_ERR_ARG, "null pointer");
+    if (T < 1 || h0 < 1 || w0 < 1) return fail(DM_ERR_ARG, "empty batch (T=%d, h0=%d, w0=%d)", T, h0, w0);
+    if (nlev < 2) return fail(DM_ERR_SHAPE, "list index out of range: Matching._B needs >= 2 levels (got %d)", nlev);
+    if (nlev > 31) return fail(DM_ERR_ARG, "too many levels %d", nlev);
+    const int K = nlev - 1;
+    if ((h0 >> K) << K != h0 || (w0 >> K) << K != w0)
+        return fail(DM_ERR_SHAPE, "map sides %dx%d not divisible by 2^(nlev-1) (nlev=%d)", h0, w0, nlev);
+    for (int l = 1; l < nlev; ++l)
+        if (!d_levels[l]) return fail(DM_ERR_ARG, "null level pointer %d", l);
+    if (filter_num > 0 && (filter_window < 1 || filter_window > 7))
+        return fail(DM_ERR_UNSUPPORTED, "filter_window_size %d not in [1, 7]", filter_window);
+    if (filter_mode != 0 && filter_mode != 1) return fail(DM_ERR_ARG, "invalid filtering mode %d", filter_mode);
+    Geo g{};
+    Stats s{};
+    if (!d_levels[0]) {
+        int rc = check_tiles(b);
+        if (rc) return rc;
+        if (!d_stats) return fail(DM_ERR_ARG, "level 0 on demand needs the statistics workspace");
+        if (b->T != T || b->h0 != h0 || b->w0 != w0) return fail(DM_ERR_ARG, "tile batch does not match T/h0/w0");
+        g = make_geo(b);
+        s = stats_view((void *)d_stats, T, h0 * w0);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    double *buf[2] = {d_out, d_scratch};
+    int cur = 0;
+    int h = h0 >> K, w = w0 >> K;
+    int fleft = filter_num;
+    auto filt = [&](int hh, int ww) -> int { // Matching._filter hook (:91-93, :136-138)
+        if (fleft > 0) {
+            if (hh >= filter_window && ww >= filter_window) {
+                if (hh != ww) return fail(DM_ERR_UNSUPPORTED, "Matching._filter needs square maps (%dx%d): Matching.py:235-236", hh, ww);
+                k_filter<<<nblk((size_t)T * hh * ww, 64), 64, 0, st>>>(buf[cur], buf[cur ^ 1], T, hh, ww, filter_window, filter_mode);
+                HIP_TRY(hipGetLastError());
+                cur ^= 1;
+            }
+            --fleft; // decremented even when the size check skips the filter
+        }
+        return DM_OK;
+    };
+    k_match_top<<<nblk((size_t)T * h * w, 64), 64, 0, st>>>(d_levels[K], T, h, w, buf[cur]);
+    HIP_TRY(hipGetLastError());
+    int rc = filt(h, w);
+    if (rc) return rc;
+    for (int l = K - 1; l >= 0; --l) {
+        const size_t n = (size_t)T * (2 * h) * (2 * w);
+        k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], T, h, w, buf[cur], buf[cur ^ 1]);
+        HIP_TRY(hipGetLastError());
+        cur ^= 1;
+        h *= 2; w *= 2;
+        rc = filt(h, w);
+        if (rc) return rc;
+    }
+    if (sub_pix) {
+        k_subpix<<<nblk((size_t)T * h0 * w0, 64), 64, 0, st>>>(g, s, d_levels[0], T, h0, w0, buf[cur]);
+        HIP_TRY(hipGetLastError());
+    }
+    if (buf[cur] != d_out)
+        HIP_TRY(hipMemcpyAsync(d_out, buf[cur], sizeof(double) * 3 * (size_t)T * h0 * w0, hipMemcpyDeviceToDevice, st));
+    return DM_OK;
+}
+
+int dm_sub_pix_cal(const double *d_arr, const double *d_score, int32_t h, int32_t w, int32_t direction,
+                   double ratio, double *d_out, void *stream)
+{
+    if (!d_arr || !d_score || !d_out || h < 1 || w < 1) return fail(DM_ERR_ARG, "bad sub_pix_cal arguments");
+    if (direction != 0 && direction != 1) return fail(DM_ERR_ARG, "direction must be 0 or 1 (got %d)", direction);
+    const size_t n = (size_t)h * w;
+    k_sub_pix_cal<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_arr, d_score, h, w, direction, ratio, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_cal_map(const double *d_map, int32_t T, int32_t h, int32_t w, int32_t mode, double *d_out, void *stream)
+{
+    if (!d_map || !d_out || T < 1 || h < 1 || w < 1) return fail(DM_ERR_ARG, "bad cal_map arguments");
+    if (mode < 0 || mode > 2) return fail(DM_ERR_ARG, "please input valid mode! (%d)", mode);
+    const size_t n = (size_t)T * h * w;
+    k_cal_map<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_map, T, h, w, mode, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_stitch(const double *d_match, int32_t n0, int32_t n1, int32_t h0, int32_t w0, int32_t stride0,
+              int32_t stride1, const int32_t *modes, int32_t nmodes, double *d_dmap, double *d_score,
+              void *stream)
+{
+    if (!d_match || !d_dmap || !d_score || n0 < 1 || n1 < 1 || stride0 < 1 || stride1 < 1 ||
+        nmodes < 0 || nmodes > 8 || (nmodes && !modes))
+        return fail(DM_ERR_ARG, "bad stitch arguments");
+    Modes m;
+    for (int k = 0; k < 8; ++k) m.m[k] = k < nmodes ? modes[k] : 0;
+    for (int k = 0; k < nmodes; ++k)
+        if (m.m[k] < 0 || m.m[k] > 2) return fail(DM_ERR_ARG, "please input valid mode! (%d)", m.m[k]);
+    const int Hout = stride0 * (n0 - 1) + h0, Wout = stride1 * (n1 - 1) + w0;
+    const size_t n = (size_t)Hout * Wout;
+    k_stitch<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_match, n0, n1, h0, w0, stride0, stride1, m,
+                                                            nmodes, d_dmap, d_score, Hout, Wout);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,270 @@
+"""Device-resident correlation engine: batches of equally sized tiles -> pyramid -> matches.
+
+This is the layer the reference-surface mirror (``misc/``) and the tile scheduler sit on.
+Everything stays in HBM as torch tensors; the HIP library (``_lib``) is called with raw
+device pointers on the current torch stream.  Reference call stack it replaces:
+``Correlation_map.__call__`` (misc/Correlation_map.py:161-173) ->
+``Matching.__call__`` (misc/Matching.py:211-222) -> ``Calc_difference.cal_map``
+(misc/Calc_difference.py:26-49), per tile of ``ImageCutSolver`` (misc/image_cut_solver.py).
+"""
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+LAM = 1.4
+
+
+def default_device():
+    if not torch.cuda.is_available():
+        raise L.DmUnavailable('no HIP device visible: the engine runs on MI355X only')
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def pyramid_plan(h0, w0):
+    """Level count and N_map of Correlation_map._multi_level_correlation_pyramid
+    (misc/Correlation_map.py:143-156).  Raises where its _aggregation would (:96-103)."""
+    N, it, h, w = 1, 1, h0, w0
+    while N < min(h0, w0):
+        if h % 2 or w % 2:
+            raise ValueError('could not broadcast input array from shape (%d,%d) into shape '
+                             '(%d,%d)' % ((h + 1) // 2, (w + 1) // 2, h // 2, w // 2))
+        h, w, N, it = h // 2, w // 2, N * 2, it + 1
+    return it, N
+
+
+def to_device_u8(img, device):
+    if isinstance(img, torch.Tensor):
+        t = img
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(img, dtype=np.uint8)))
+    if t.dtype != torch.uint8 or t.dim() != 2:
+        raise ValueError('images must be 2-D uint8')
+    return t.to(device).contiguous()
+
+
+class TileBatch:
+    """T tiles of one image pair: tile t is the (h0+ws-1) x (w0+ws-1) crop at origins[t]."""
+
+    def __init__(self, img1, img2, origins, h0, w0, ws, method, device=None):
+        self.device = device or default_device()
+        self.img1 = to_device_u8(img1, self.device)
+        self.img2 = to_device_u8(img2, self.device)
+        if self.img1.shape != self.img2.shape:
+            raise ValueError('img1 and img2 must have the same shape')
+        org = np.asarray(origins, dtype=np.int64).reshape(-1, 2)
+        H, W = self.img1.shape
+        if ws < 1 or ws % 2 == 0:
+            raise ValueError('could not broadcast: window_size must be odd (got %d)' % ws)
+        if len(org) == 0 or h0 < 1 or w0 < 1:
+            raise ValueError('empty tile batch')
+        # the kernels trust these bounds: check them here, on the host
+        if org.min() < 0 or (org[:, 0] + h0 + ws - 1).max() > H or (org[:, 1] + w0 + ws - 1).max() > W:
+            raise ValueError('tile crop outside the image')
+        self.origins_host = org
+        self.origins = torch.from_numpy(org.astype(np.int32)).to(self.device).contiguous()
+        self.T, self.h0, self.w0, self.ws, self.method = len(org), int(h0), int(w0), int(ws), int(method)
+        self.struct = L.DmTiles(self.img1.data_ptr(), self.img2.data_ptr(),
+                                self.img1.stride(0), self.img2.stride(0),
+                                self.origins.data_ptr(), self.T, self.h0, self.w0,
+                                self.ws, self.method)
+
+    @property
+    def P(self):
+        return self.h0 * self.w0
+
+    def ref(self):
+        return ctypes.byref(self.struct)
+
+
+class DevicePyramid:
+    """co_map_list of a TileBatch, resident on the device.
+
+    levels[0] is not stored (the fused kernel never writes level 0; matching evaluates it
+    on demand); levels[l] for l >= 1 are float64 [T][Pl][Pl] tensors."""
+
+    def __init__(self, batch, stream=None, build=True):
+        self.b = batch
+        self.lib = L.load()
+        self.nlev, self.N_map = pyramid_plan(batch.h0, batch.w0)
+        self.stream = stream
+        self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
+                                 device=batch.device)
+        self.levels = [None]
+        self._volume = None
+        self._have_minmax = False
+        self._have_stats = False
+        if build:
+            self.build()
+
+    def _s(self):
+        return L.stream_handle(self.stream)
+
+    def compute_stats(self):
+        if not self._have_stats:
+            L.check(self.lib.dm_corr_stats(self.b.ref(), L.ptr(self.stats), self._s()),
+                    'dm_corr_stats')
+            self._have_stats = True
+        return self
+
+    def build(self):
+        b, lib = self.b, self.lib
+        self.compute_stats()
+        if self.nlev > 1 and len(self.levels) == 1:
+            P1 = (b.h0 // 2) * (b.w0 // 2)
+            l1 = torch.empty((b.T, P1, P1), dtype=torch.float64, device=b.device)
+            L.check(lib.dm_corr_level1(b.ref(), L.ptr(self.stats), L.ptr(l1), self._s()),
+                    'dm_corr_level1')
+            self.levels.append(l1)
+            self._have_minmax = True
+            h, w = b.h0 // 2, b.w0 // 2
+            for _ in range(2, self.nlev):
+                P2 = (h // 2) * (w // 2)
+                nxt = torch.empty((b.T, P2, P2), dtype=torch.float64, device=b.device)
+                L.check(lib.dm_aggregate(L.ptr(self.levels[-1]), b.T, h, w, 1, L.ptr(nxt),
+                                         self._s()), 'dm_aggregate')
+                self.levels.append(nxt)
+                h, w = h // 2, w // 2
+        return self
+
+    def level_shape(self, k):
+        h, w = self.b.h0 >> k, self.b.w0 >> k
+        return (h, w, h, w)
+
+    def volume(self):
+        """Level-0 min-max volume (co_map before rectification), float32 [T][P][P]."""
+        if self._volume is None:
+            self.compute_stats()
+            b = self.b
+            v = torch.empty((b.T, b.P, b.P), dtype=torch.float32, device=b.device)
+            L.check(self.lib.dm_corr_volume(b.ref(), L.ptr(self.stats), L.ptr(v), self._s()),
+                    'dm_corr_volume')
+            self._have_minmax = True
+            self._volume = v
+        return self._volume
+
+    def level(self, k):
+        """co_map_list[k] as a float64 device tensor [T][Pk][Pk]."""
+        if k < 0:
+            k += self.nlev
+        if not 0 <= k < self.nlev:
+            raise IndexError('list index out of range')
+        if k > 0:
+            return self.levels[k]
+        v = self.volume()
+        out = torch.empty(v.shape, dtype=torch.float64, device=v.device)
+        L.check(self.lib.dm_rectify(L.ptr(v), v.numel(), L.ptr(out), self._s()), 'dm_rectify')
+        return out
+
+    def match(self, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
+              filtering_mode='median'):
+        """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score)."""
+        b = self.b
+        if not self._have_minmax:
+            self.volume()
+        out = torch.empty((b.T, 3, b.h0, b.w0), dtype=torch.float64, device=b.device)
+        scratch = torch.empty_like(out)
+        ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [t.data_ptr() for t in self.levels[1:]]))
+        fnum = int(filtering_num) if filtering else 0
+        L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, self.nlev, b.T, b.h0, b.w0,
+                                  int(bool(sub_pix)), int(filter_window_size), fnum,
+                                  1 if filtering_mode == 'median' else 0,
+                                  L.ptr(scratch), L.ptr(out), self._s()), 'dm_match')
+        return out
+
+
+def match_levels(levels, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
+                 filtering_mode='median', device=None):
+    """Matching on an arbitrary (host or device) co_map_list, level 0 materialised."""
+    device = device or default_device()
+    lib = L.load()
+    lv = [torch.as_tensor(np.ascontiguousarray(x) if not isinstance(x, torch.Tensor) else x,
+                          dtype=torch.float64).to(device).contiguous() for x in levels]
+    h0, w0 = lv[0].shape[:2]
+    out = torch.empty((1, 3, h0, w0), dtype=torch.float64, device=device)
+    scratch = torch.empty_like(out)
+    ptrs = (ctypes.c_void_p * len(lv))(*[t.data_ptr() for t in lv])
+    fnum = int(filtering_num) if filtering else 0
+    L.check(lib.dm_match(None, None, ptrs, len(lv), 1, h0, w0, int(bool(sub_pix)),
+                         int(filter_window_size), fnum, 1 if filtering_mode == 'median' else 0,
+                         L.ptr(scratch), L.ptr(out), L.stream_handle()), 'dm_match')
+    return out[0]
+
+
+def cal_map(match, mode, stream=None):
+    """Calc_difference.cal_map on a [T][3][h][w] (or [3][h][w]) device tensor."""
+    if mode not in L.CAL_MODES:
+        raise ValueError(mode)
+    m = match if match.dim() == 4 else match[None]
+    m = m.contiguous()
+    T, _, h, w = m.shape
+    out = torch.empty((T, h, w), dtype=torch.float64, device=m.device)
+    L.check(L.load().dm_cal_map(L.ptr(m), T, h, w, L.CAL_MODES[mode], L.ptr(out),
+                                L.stream_handle(stream)), 'dm_cal_map')
+    return out if match.dim() == 4 else out[0]
+
+
+# ----------------------------------------------------------------------------------------
+# tile scheduler (ImageCutSolver semantics, misc/image_cut_solver.py:58-179)
+# ----------------------------------------------------------------------------------------
+def cut_grid(shape, image_size, stride, window_size):
+    """Tile counts and origins in the reference order (j outer, i inner; :62, :103-113)."""
+    ex = int((window_size - 1) / 2)
+    trimmed = [image_size[i] + 2 * ex for i in range(2)]
+    n = [int(np.floor((shape[i] - trimmed[i]) / stride[i])) for i in range(2)]
+    if n[0] < 1 or n[1] < 1:
+        raise IndexError('list index out of range (no tile fits: image_cut_solver.py:150)')
+    org = [(stride[0] * i, stride[1] * j) for j in range(n[1]) for i in range(n[0])]
+    return n, np.array(org, dtype=np.int64)
+
+
+def tile_bytes(h0, w0):
+    """Device bytes one tile needs inside DevicePyramid + match (levels >= 1, stats, maps)."""
+    nlev, _ = pyramid_plan(h0, w0)
+    P = h0 * w0
+    total = 6 * 4 * P + 2 * 3 * 8 * P
+    h, w = h0, w0
+    for _ in range(1, nlev):
+        h, w = h // 2, w // 2
+        total += 8 * (h * w) ** 2
+    return total
+
+
+def solve_tiles(img1, img2, origins, h0, w0, ws, method, sub_pix=True, filtering=False,
+                filter_window_size=3, filtering_num=3, filtering_mode='median',
+                device=None, mem_budget=None, stream=None):
+    """Correlation_map + Matching for every tile; float64 [T][3][h0][w0] device tensor.
+    Tiles are processed in chunks that fit ``mem_budget`` bytes of HBM."""
+    device = device or default_device()
+    img1 = to_device_u8(img1, device)
+    img2 = to_device_u8(img2, device)
+    origins = np.asarray(origins, dtype=np.int64).reshape(-1, 2)
+    if mem_budget is None:
+        mem_budget = int(os.environ.get('DM_MEM_BUDGET', 64 << 30))
+    per = tile_bytes(h0, w0)
+    chunk = max(1, min(len(origins), mem_budget // max(per, 1)))
+    out = torch.empty((len(origins), 3, h0, w0), dtype=torch.float64, device=device)
+    for s in range(0, len(origins), chunk):
+        b = TileBatch(img1, img2, origins[s:s + chunk], h0, w0, ws, method, device)
+        pyr = DevicePyramid(b, stream=stream)
+        out[s:s + len(b.origins_host)] = pyr.match(sub_pix, filtering, filter_window_size,
+                                                   filtering_num, filtering_mode)
+        del pyr, b
+    return out
+
+
+def stitch(match, n, h0, w0, stride, modes, stream=None):
+    """ImageCutSolver._execute_matching stitching on the device -> (d_map, out_map)."""
+    mode_ids = [L.CAL_MODES[m] for m in modes]
+    Hout, Wout = stride[0] * (n[0] - 1) + h0, stride[1] * (n[1] - 1) + w0
+    dmap = torch.empty((len(modes), Hout, Wout), dtype=torch.float64, device=match.device)
+    score = torch.empty((Hout, Wout), dtype=torch.float64, device=match.device)
+    arr = (ctypes.c_int32 * max(1, len(mode_ids)))(*mode_ids)
+    L.check(L.load().dm_stitch(L.ptr(match.contiguous()), n[0], n[1], h0, w0, stride[0],
+                               stride[1], arr, len(mode_ids), L.ptr(dmap), L.ptr(score),
+                               L.stream_handle(stream)), 'dm_stitch')
+    return dmap, score

@@ -1,0 +1,99 @@
+"""Matching mirror (reference: misc/Matching.py:20-268), backtracking on gfx950 kernels.
+
+``__call__`` runs the whole coarse-to-fine descent (_initial_move_map, _B / _calc_match,
+optional _filter, _sub_pix_cal) in dm_match.  On a GPU-backed ``Correlation_map`` level 0
+is re-evaluated on demand from the images (never materialised); for any other object
+with a ``co_map_list`` the levels are uploaded and matched as given.
+"""
+
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import engine
+
+
+class Matching():
+    '''
+    multi-level correlation pyramidからマッチングを行う
+    原著の14式に従って計算していく
+    '''
+
+    def __init__(
+        self,
+        Co_obj=None,
+        filter_window_size=3,
+        filtering=False,
+        filtering_num=3,
+        filtering_mode='median',
+        sub_pix=True
+    ):
+        try:
+            Co_obj.co_map_list
+        except AttributeError as e:
+            print('Error!: {}'.format(e))
+            print('please run \'obj=Correlation_map()\' and \'obj()\' first.')
+            sys.exit()
+
+        MODES = ['average', 'median']
+        assert filtering_mode in MODES, 'invalid filtering mode is input!: {}'.format(filtering_mode)
+
+        self.obj = Co_obj
+        self.Padding = Zero_padding()
+        self.Padding.eval()
+
+        self.filtering_num = filtering_num
+        self.filter_window_size = filter_window_size
+        self.filtering = filtering
+        self.filtering_mode = filtering_mode
+        self.sub_pix = sub_pix
+
+    @classmethod
+    def _sub_pix_compute(self, r0, r1, r_):
+        '''
+        二次関数近似の計算 (vertex of the parabola through r_, r0, r1; 0 if r0 is not a
+        strict maximum).  Scalar helper; the kernel k_subpix evaluates the same expression.
+        '''
+        if r0 > r1 and r0 > r_:
+            diff = - (r1 - r_) / (2 * (r1 + r_ - 2 * r0))
+        else:
+            diff = 0
+        return diff
+
+    def _device_match(self):
+        pyr = getattr(self.obj, '_pyr', None)
+        nlev = len(self.obj.co_map_list)
+        fnum = self.filtering_num if self.filtering else 0
+        if isinstance(pyr, engine.DevicePyramid):
+            out = pyr.match(self.sub_pix, self.filtering, self.filter_window_size, fnum,
+                            self.filtering_mode)[0]
+        else:
+            out = engine.match_levels(list(self.obj.co_map_list), self.sub_pix, self.filtering,
+                                      self.filter_window_size, fnum, self.filtering_mode)
+        if self.filtering:  # _initial_move_map / _B decrement it once per level (:91-93, :136-138)
+            self.filtering_num = max(0, self.filtering_num - nlev)
+        return out
+
+    def __call__(self):
+        '''
+        multi-level correlation pyramidからマッチング計算を行う
+        -> float64 (3, H', W'): matched row, matched col (sub-pixel if sub_pix), score
+        '''
+        self.map = self._device_match().cpu().numpy()
+        return self.map
+
+
+class Zero_padding(nn.Module):
+    '''
+    原著の14式の計算のため、ゼロパディングしておく (API compatibility; the matching kernel
+    reads out-of-range window cells as 0 instead of padding each map)
+    '''
+
+    def __init__(self):
+        super(Zero_padding, self).__init__()
+        self.m = nn.ZeroPad2d(1)
+
+    def forward(self, x):
+        return self.m(x)

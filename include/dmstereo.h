@@ -1,0 +1,151 @@
+/*
+ * dmstereo.h -- C ABI of the MI355X (gfx950) DeepMatching stereo correlation engine.
+ *
+ * The reference path this ABI replaces is Python (Yuki-Kumon/deepmatching_stereo_matching):
+ *   misc/Correlation_map.py  Correlation_map (:29-173), Maxpool (:176-184)
+ *   misc/Feature_value.py    Feature_value (:18-43) -> cv2.matchTemplate + min_max
+ *   misc/Matching.py         Matching (:20-255), Zero_padding (:258-268)
+ *   misc/Calc_difference.py  Calc_difference.cal_map (:26-49)
+ *   misc/sub_pix_cal.py      sub_pix_cal (:22-53)
+ *   misc/image_cut_solver.py ImageCutSolver._execute_matching stitching (:144-179)
+ * The Python mirror of that surface (deepmatching_stereo_matching_amd/misc/) binds
+ * these entry points with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every pointer argument named d_* is DEVICE memory owned by the caller (torch
+ *    tensors in the Python host).  The library never allocates or frees device memory
+ *    and keeps no global mutable state besides a per-thread error string.
+ *  - Work is enqueued on `stream` (a hipStream_t passed as void*; NULL = default stream)
+ *    and is asynchronous; nothing here synchronises.
+ *  - Return 0 (DM_OK) or a negative dm_status; dm_last_error() describes the failure.
+ *
+ * Shapes.  A batch holds T tiles of equal size cut from one image pair.  For tile t the
+ * crop is rows [org_t.r, org_t.r + h0 + ws - 1) x cols [org_t.c, org_t.c + w0 + ws - 1) of
+ * img1 and img2 (the same window in both, as ImageCutSolver._cut_and_pool does,
+ * image_cut_solver.py:95-113).  h0 = H' and w0 = W' are the correlation-map sides
+ * (Correlation_map: H' = H - 2*exclusive_pix).  P = h0*w0.
+ *  level 0  : "co_map", float32 [T][P][P] (min-max normalised, NOT rectified)
+ *  level l>0: float64 [T][Pl][Pl], Pl = (h0>>l)*(w0>>l), rectified (**1.4) like
+ *             co_map_list[l].
+ */
+#ifndef DMSTEREO_H
+#define DMSTEREO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum dm_status {
+    DM_OK = 0,
+    DM_ERR_ARG = -1,         /* bad pointer / size argument                              */
+    DM_ERR_SHAPE = -2,       /* shape the reference cannot process (even ws, odd sides) */
+    DM_ERR_UNSUPPORTED = -3, /* valid for the reference, not (yet) for this engine      */
+    DM_ERR_HIP = -4          /* a HIP runtime call failed                               */
+};
+
+enum dm_method { /* cv2 constants, Feature_value.py:23-30 */
+    DM_TM_CCOEFF = 4,
+    DM_TM_CCOEFF_NORMED = 5
+};
+
+enum dm_cal_mode { /* Calc_difference.cal_map modes, Calc_difference.py:30 */
+    DM_CAL_ELEVATION = 0,  /* j - map[1] */
+    DM_CAL_ELEVATION2 = 1, /* i - map[0] */
+    DM_CAL_DISTANCE = 2    /* || (i, j) - map[:2] || */
+};
+
+typedef struct dm_tiles {
+    const uint8_t *d_img1;    /* "img" / original / before   (Correlation_map arg 1) */
+    const uint8_t *d_img2;    /* "template" / after          (Correlation_map arg 2) */
+    int32_t pitch1, pitch2;   /* row pitch in bytes                                   */
+    const int32_t *d_origins; /* [T][2] crop top-left (row, col)                      */
+    int32_t T;                /* tiles in the batch                                    */
+    int32_t h0, w0;           /* correlation-map sides                                 */
+    int32_t ws;               /* window_size, odd, 1..15                               */
+    int32_t method;           /* dm_method                                             */
+} dm_tiles;
+
+/* Size in bytes of the per-batch statistics workspace (per-patch / per-window moments,
+ * per-patch min/max of the level-0 map): 6 * 4 * T * P. */
+size_t dm_stats_bytes(const dm_tiles *b);
+
+/* Per-patch and per-window moments.
+ * Replaces Correlation_map._create_atomic_patch (Correlation_map.py:51-67) and the
+ * template/window sums inside cv2.matchTemplate (Feature_value.py:41). */
+int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream);
+
+/* Level-0 ZNCC + per-patch min-max + rectification + MaxPool(3,2,1) + 4-child average +
+ * rectification, fused: writes level 1 (float64 [T][P1][P1]) and the per-patch min/max
+ * into d_stats.  Level 0 is never written.
+ * Replaces Correlation_map._create_simple_initial_co_map (:69-87), Feature_value.min_max
+ * (Feature_value.py:32-37), _rectification (:158-159) and the first _aggregation
+ * (:89-130) of _multi_level_correlation_pyramid (:132-156).  Needs dm_corr_stats first. */
+int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *stream);
+
+/* Materialise the level-0 min-max volume "co_map" (float32 [T][P][P]) and the per-patch
+ * min/max.  Replaces _create_simple_initial_co_map (:69-87) for callers that read
+ * co_map directly (bad_matching.py:62-70).  Needs dm_corr_stats first. */
+int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream);
+
+/* d_out[i] = d_in[i] ** 1.4 (pinned float64 pow, dm_pow.h).  Replaces
+ * Correlation_map._rectification (:158-159) for the materialised co_map_list[0]. */
+int dm_rectify(const float *d_in, size_t n, double *d_out, void *stream);
+
+/* Same for float64 input (Correlation_map._rectification on an aggregated map). */
+int dm_rectify64(const double *d_in, size_t n, double *d_out, void *stream);
+
+/* One pyramid step for levels >= 1: MaxPool2d(3,2,1) per map, (ul+ur+ll+lr)/4, and
+ * (rectify != 0) the 1.4 power.  d_in float64 [T][h*w][h*w] -> d_out float64
+ * [T][(h/2)*(w/2)][(h/2)*(w/2)].
+ * Replaces Correlation_map._aggregation (:89-130) [+ _rectification (:148)]. */
+int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t rectify,
+                 double *d_out, void *stream);
+
+/* Coarse-to-fine matching on a pyramid of nlev levels of T tiles with level-0 sides
+ * h0 x w0.  d_levels is a HOST array of nlev device pointers to float64 rectified levels
+ * (co_map_list).  d_levels[0] may be NULL: level 0 is then evaluated on demand from the
+ * images and the statistics (b and d_stats required; b->T/h0/w0 must match).
+ * filter_num > 0 runs Matching._filter (:224-255; filter_mode 0 average, 1 median, window
+ * filter_window <= 7, square maps only) after the top level and after each _B step while
+ * the count lasts, as Matching._initial_move_map / _B do.
+ * d_scratch: float64 [T][3][h0*w0].  d_out: float64 [T][3][h0][w0] = (row, col, score),
+ * as returned by Matching.__call__ (Matching.py:211-222): _initial_move_map (:80-96),
+ * _B/_calc_match (:98-149), _calc_near_match (:58-78), _sub_pix_cal (:177-209). */
+int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_levels,
+             int32_t nlev, int32_t T, int32_t h0, int32_t w0, int32_t sub_pix,
+             int32_t filter_window, int32_t filter_num, int32_t filter_mode,
+             double *d_scratch, double *d_out, void *stream);
+
+/* misc/sub_pix_cal.py sub_pix_cal (:22-53): clamp to [-3,3], quadratic refinement of an
+ * (h, w) disparity map along `direction` (0 rows, 1 cols) on the score map scaled by
+ * `ratio`, reject |delta| > 1, clamp again.  float64 in/out, device pointers. */
+int dm_sub_pix_cal(const double *d_arr, const double *d_score, int32_t h, int32_t w,
+                   int32_t direction, double ratio, double *d_out, void *stream);
+
+/* Calc_difference.cal_map (Calc_difference.py:26-49) on T maps [T][3][h][w] -> [T][h][w]. */
+int dm_cal_map(const double *d_map, int32_t T, int32_t h, int32_t w, int32_t mode,
+               double *d_out, void *stream);
+
+/* ImageCutSolver stitching (image_cut_solver.py:144-179): tiles t = j*n0 + i of d_match
+ * ([T][3][h0][w0]) are written at (stride0*i, stride1*j), later tiles overwriting
+ * earlier ones.  d_dmap: [nmodes][Hout][Wout] (cal_map of each mode in `modes`, a HOST
+ * array), d_score: [Hout][Wout] (map[2]).  Hout = stride0*(n0-1)+h0, likewise Wout.
+ * Output cells no tile covers are NaN (np.empty garbage in the reference). */
+int dm_stitch(const double *d_match, int32_t n0, int32_t n1, int32_t h0, int32_t w0,
+              int32_t stride0, int32_t stride1, const int32_t *modes, int32_t nmodes,
+              double *d_dmap, double *d_score, void *stream);
+
+/* Human-readable description of the last failure on this thread. */
+const char *dm_last_error(void);
+
+/* ABI version (major * 100 + minor). */
+int dm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DMSTEREO_H */

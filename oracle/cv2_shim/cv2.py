@@ -15,7 +15,9 @@ argument-swap rule and with the *pinned* arithmetic that the C oracle
     dT   = n*sum(T*T) - sum(T)**2 ; dI likewise           exact integer
     NORMED:  dT == 0           -> r = 1.0 for every window (OpenCV: templNorm < eps)
              a = f32(1/sqrt(f64 dT)),  b = 0 if dI == 0 else f32(1/sqrt(f64 dI))
-             r = clamp(f32(num) * f32(a*b), -1, 1)        all products in float32
+             y = f32(num) * b ;  r = clamp(y * a, -1, 1)   products rounded to float32
+             (b first, a last: r is then a monotone function of y for a fixed patch, which
+             the kernels use to pool and min/max on y -- see DESIGN.md)
     CCOEFF:  r = f32(num) * f32(1/n)
 
 OpenCV 3.4.1 itself (``environment.yml:15``) correlates in float32 via DFT/IPP and is
@@ -65,6 +67,6 @@ def matchTemplate(image, templ, method):
     with np.errstate(divide='ignore'):
         b = (1.0 / np.sqrt(dI.astype(np.float64))).astype(np.float32)
     b[dI == 0] = np.float32(0.0)
-    c = (a * b).astype(np.float32)
-    r = (numf * c).astype(np.float32)
+    y = (numf * b).astype(np.float32)
+    r = (y * a).astype(np.float32)
     return np.clip(r, np.float32(-1.0), np.float32(1.0)).astype(np.float32)

@@ -90,8 +90,8 @@ int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
                 } else if (dT == 0) {
                     r = 1.0f;
                 } else {
-                    const float c = a * bq[q];
-                    r = (float)num * c;
+                    const float y = (float)num * bq[q];
+                    r = y * a;
                     r = r < -1.0f ? -1.0f : (r > 1.0f ? 1.0f : r);
                 }
                 row[q] = r;

@@ -1,0 +1,213 @@
+"""GPU parity: the HIP path (through the C ABI, via the reference-surface mirror and the
+batched engine) against the CPU oracle and the reference's golden fixtures.
+
+The oracle runs with the pinned pow (dm_pow.h, the one the kernels evaluate), so every
+output -- float32 level 0, float64 levels, integer correspondences, sub-pixel values,
+scores, cal_map -- must match it BIT FOR BIT.  Against the reference fixtures the
+tolerances of test_oracle_golden.py apply (float64 pow is platform-dependent there).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+PAIRS = sorted(glob.glob(os.path.join(GOLD, 'pair_*.npz')))
+TOL_F64 = 1e-12
+TOL_SUBPIX = 1e-9
+
+
+def _same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert np.array_equal(a, b, equal_nan=True), 'max |d| = %r' % np.nanmax(np.abs(a - b))
+
+
+def _close(a, b, tol):
+    assert a.shape == b.shape
+    na, nb = np.isnan(a), np.isnan(b)
+    assert np.array_equal(na, nb)
+    if (~na).any():
+        assert np.max(np.abs(a[~na] - b[~na])) <= tol
+
+
+@pytest.fixture(scope='module', autouse=True)
+def pinned_pow():
+    assert torch.cuda.is_available(), 'GPU tests need the MI355X'
+    O.set_pow_mode('pinned')
+    yield
+    O.set_pow_mode('libm')
+
+
+@pytest.fixture(scope='module')
+def mirror():
+    from deepmatching_stereo_matching_amd.misc import Correlation_map, Matching, Calc_difference
+    return Correlation_map, Matching, Calc_difference
+
+
+@pytest.fixture(scope='module', params=PAIRS, ids=lambda p: os.path.basename(p)[:-4])
+def case(request, mirror):
+    CM, MT, CD = mirror
+    g = dict(np.load(request.param))
+    ws, feat = int(g['ws']), str(g['feature'])
+    co = CM.Correlation_map(g['img1'], g['img2'], window_size=ws, feature_name=feat)
+    co()
+    ol0 = O.corr_l0(g['img1'], g['img2'], ws, feat)
+    olev, it, n_map = O.pyramid(ol0)
+    return g, co, ol0, olev, it, n_map
+
+
+def test_level0_volume_bit_exact(case):
+    g, co, ol0, *_ = case
+    l0 = co.co_map.astype(np.float32)
+    _same(l0, ol0)
+    if 'l0' in g:
+        _same(l0, g['l0'])
+
+
+def test_pyramid_bit_exact(case):
+    g, co, ol0, olev, it, n_map = case
+    assert co.iteration == it == int(g['iteration'])
+    assert co.N_map == n_map == int(g['N_map'])
+    assert len(co.co_map_list) == len(olev)
+    for k in range(len(olev)):
+        _same(co.co_map_list[k], olev[k])
+        if 'level%d' % k in g:
+            _close(co.co_map_list[k], g['level%d' % k], TOL_F64)
+
+
+def test_matching_bit_exact(case, mirror):
+    CM, MT, CD = mirror
+    g, co, ol0, olev, *_ = case
+    m = MT.Matching(co, sub_pix=False)()
+    _same(m, O.match(olev, sub_pix=False))
+    assert np.array_equal(m[:2], g['match'][:2])
+    ms = MT.Matching(co)()
+    _same(ms, O.match(olev, sub_pix=True))
+    _close(ms, g['match_subpix'], TOL_SUBPIX)
+    for mode in ('elevation', 'elevation2', 'distance'):
+        d = CD.Calc_difference.cal_map(ms, mode=mode)
+        _same(d, O.cal_map(ms, mode))
+        _close(d, g['calmap_' + mode], TOL_SUBPIX)
+
+
+def test_matching_filtered(case, mirror):
+    CM, MT, CD = mirror
+    g, co, ol0, olev, *_ = case
+    for fm in ('median', 'average'):
+        if 'match_filter_' + fm in g:
+            m = MT.Matching(co, filtering=True, filtering_mode=fm, filtering_num=3)()
+            _same(m, O.match(olev, sub_pix=True, filtering=True, filtering_mode=fm, filtering_num=3))
+            _close(m, g['match_filter_' + fm], TOL_SUBPIX)
+
+
+def test_matching_on_materialised_levels(case, mirror):
+    """Matching on a foreign co_map_list (plain numpy levels, level 0 materialised)."""
+    CM, MT, CD = mirror
+    g, co, ol0, olev, *_ = case
+
+    class Plain:
+        co_map_list = olev
+    _same(MT.Matching(Plain())(), O.match(olev, sub_pix=True))
+
+
+def test_private_methods(case, mirror):
+    CM, MT, CD = mirror
+    g, co, ol0, olev, *_ = case
+    if len(olev) > 2:
+        _same(co._rectification(co._aggregation(olev[1])), olev[2])
+    _same(co._rectification(ol0), olev[0])
+
+
+@pytest.mark.parametrize('name', ['cut_44_s16_st12', 'cut_52x40_s16_pad'])
+def test_image_cut_solver(name):
+    from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+    g = np.load(os.path.join(GOLD, name + '.npz'))
+    modes = ['elevation', 'elevation2', 'distance'][:g['d_map'].shape[0]]
+    pad = name.endswith('_pad')
+    kw = dict(image_size=list(g['image_size']), stride=list(g['stride']), window_size=int(g['ws']),
+              degree_map_mode=modes, padding=pad)
+    d_map, score = ImageCutSolver(g['img1'], g['img2'], **kw)()
+    od, os_ = O.cut_solve(g['img1'], g['img2'], **kw)
+    _same(d_map, od)
+    _same(score, os_)
+    covered = ~np.isnan(score)
+    _close(d_map[:, covered], g['d_map'][:, covered], TOL_SUBPIX)
+    _close(score[covered], g['score'][covered], TOL_F64)
+
+
+def test_sub_pix_cal():
+    from deepmatching_stereo_matching_amd.misc.sub_pix_cal import sub_pix_cal
+    g = np.load(os.path.join(GOLD, 'subpixcal_s32.npz'))
+    for args, key in (((0, 100.), 'out_dir0'), ((1, 30.), 'out_dir1')):
+        out = sub_pix_cal(g['arr'], g['co_map'], direction=args[0], ratio=args[1])
+        _same(out, O.sub_pix_cal(g['arr'], g['co_map'], direction=args[0], ratio=args[1]))
+        _close(out, g[key], TOL_SUBPIX)
+
+
+def test_pow_bit_identical_on_device():
+    """dm_rectify64 (device pow14) == host pow14 on random, f32-exact and tiny inputs."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.random(4000), rng.random(4000).astype(np.float32).astype(np.float64),
+                        np.exp2(rng.uniform(-700, 0, 2000)), [0.0, 1.0, 0.5, np.nan]])
+    d = torch.from_numpy(x).cuda()
+    out = torch.empty_like(d)
+    L.check(L.load().dm_rectify64(L.ptr(d), d.numel(), L.ptr(out), L.stream_handle()))
+    host = np.array([O.pow14(v) for v in x])
+    _same(out.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize('S,ws,seed', [(64, 5, 31), (32, 3, 32), (128, 5, 33)])
+def test_synthetic_tile_vs_oracle(S, ws, seed, mirror):
+    """Full-size tiles (C2: S=64, C3: S=128) against the oracle, bit for bit."""
+    CM, MT, CD = mirror
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(S + ws - 1, S + ws - 1, seed=seed, dx=2, max_disp=S // 4, sinusoidal=True)
+    co = CM.Correlation_map(a, b, window_size=ws)
+    co()
+    ol0 = O.corr_l0(a, b, ws)
+    olev, _, _ = O.pyramid(ol0)
+    for k in range(1, len(olev)):
+        _same(co.co_map_list[k], olev[k])
+    _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
+
+
+def test_batched_tiles_equal_single_tiles():
+    """Batch invariance (size-independent property): one batched solve of a tile grid ==
+    solving every tile alone; and the stitched map == per-tile cal_map."""
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(164, 164, seed=40, dx=2)
+    n, org = engine.cut_grid(a.shape, [32, 32], [32, 32], 5)
+    full = engine.solve_tiles(a, b, org, 32, 32, 5, 5)
+    small = engine.solve_tiles(a, b, org, 32, 32, 5, 5, mem_budget=1)  # one tile per batch
+    _same(full.cpu().numpy(), small.cpu().numpy())
+    dmap, score = engine.stitch(full, n, 32, 32, [32, 32], ['elevation'])
+    el = engine.cal_map(full, 'elevation').cpu().numpy()
+    dm = dmap.cpu().numpy()[0]
+    for t, (r, c) in enumerate(org):
+        _same(dm[r:r + 32, c:c + 32], el[t])
+
+
+def test_shape_errors_like_reference(mirror):
+    CM, MT, CD = mirror
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (128, 128), dtype=np.uint8)
+    with pytest.raises(ValueError):             # H' = 124: _aggregation broadcast error
+        CM.Correlation_map(img, img, window_size=5)()
+    small = rng.integers(0, 256, (20, 20), dtype=np.uint8)
+    with pytest.raises(ValueError):             # even window
+        CM.Correlation_map(small, small, window_size=4)()
+    one = rng.integers(0, 256, (5, 5), dtype=np.uint8)
+    co = CM.Correlation_map(one, one, window_size=5)
+    co()
+    assert co.iteration == 1 and co.N_map == 1
+    with pytest.raises(IndexError):              # Matching._B reads co_map_list[-2]
+        MT.Matching(co)()

@@ -1,0 +1,104 @@
+"""Host-side logic that needs no GPU: pyramid plan, tile grid, loaders, the driver flags,
+and that the product path refuses to run without the HIP device (no CPU fallback)."""
+import os
+
+import numpy as np
+import pytest
+
+from deepmatching_stereo_matching_amd import engine
+from deepmatching_stereo_matching_amd import _lib as L
+
+
+@pytest.mark.parametrize('h0,w0,nlev,N', [(32, 32, 6, 32), (16, 64, 5, 16), (64, 16, 5, 16),
+                                          (8, 8, 4, 8), (1, 1, 1, 1), (2, 6, 2, 2)])
+def test_pyramid_plan(h0, w0, nlev, N):
+    assert engine.pyramid_plan(h0, w0) == (nlev, N)
+
+
+@pytest.mark.parametrize('h0,w0', [(124, 124), (6, 6), (12, 12)])
+def test_pyramid_plan_rejects_like_reference(h0, w0):
+    # misc/Correlation_map.py:96-103: MaxPool of an odd side cannot be assigned
+    with pytest.raises(ValueError, match='broadcast'):
+        engine.pyramid_plan(h0, w0)
+
+
+def test_cut_grid_reference_order():
+    # image_cut_solver.py:62 floor rule, :103-113 j outer / i inner
+    n, org = engine.cut_grid((164, 164), [32, 32], [32, 32], 5)
+    assert n == [4, 4]
+    assert org[:5].tolist() == [[0, 0], [32, 0], [64, 0], [96, 0], [0, 32]]
+    n, org = engine.cut_grid((1156, 1156), [128, 128], [128, 128], 5)
+    assert n == [8, 8] and len(org) == 64
+    n, org = engine.cut_grid((44, 44), [16, 16], [12, 12], 5)
+    assert n == [2, 2]
+
+
+def test_cut_grid_no_tile():
+    with pytest.raises(IndexError):
+        engine.cut_grid((20, 20), [32, 32], [32, 32], 5)
+
+
+def test_tile_bytes_monotone():
+    assert engine.tile_bytes(128, 128) > engine.tile_bytes(64, 64) > 0
+    # level 1 dominates: (64*64)^2 float64
+    assert engine.tile_bytes(128, 128) >= 8 * (64 * 64) ** 2
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    with pytest.raises(L.DmUnavailable):
+        engine.default_device()
+    from deepmatching_stereo_matching_amd.misc.Correlation_map import Correlation_map
+    img = np.zeros((20, 20), np.uint8)
+    with pytest.raises(L.DmUnavailable):
+        Correlation_map(img, img, window_size=5)()
+
+
+def test_reference_error_conventions():
+    from deepmatching_stereo_matching_amd.misc.Correlation_map import Correlation_map
+    from deepmatching_stereo_matching_amd.misc.Feature_value import Feature_value
+    from deepmatching_stereo_matching_amd.misc.Matching import Matching
+    from deepmatching_stereo_matching_amd.misc.Calc_difference import Calc_difference
+    with pytest.raises(SystemExit):
+        Correlation_map(np.zeros((5, 5), np.uint8), np.zeros((5, 6), np.uint8))
+    with pytest.raises(SystemExit):
+        Feature_value('cv2.TM_SQDIFF')
+    with pytest.raises(SystemExit):
+        Matching(object())
+    with pytest.raises(SystemExit):
+        Calc_difference.cal_map(np.zeros((3, 2, 2)), mode='height')
+
+    class Fake:
+        co_map_list = []
+    with pytest.raises(AssertionError):
+        Matching(Fake(), filtering_mode='mode')
+
+
+def test_raw_read(tmp_path):
+    from deepmatching_stereo_matching_amd.misc.raw_read import RawRead
+    a = np.arange(-50, 50, dtype=np.int8).reshape(10, 10)
+    p = tmp_path / 'x.raw'
+    a.tofile(p)
+    out = RawRead.read(str(p), size=(10, 10), rate=2)
+    assert out.dtype == np.uint8 and np.array_equal(out, (a * 2).astype(np.uint8))
+
+
+def test_loader_channels(tmp_path):
+    from PIL import Image
+    from deepmatching_stereo_matching_amd.misc.loader import Loader
+    rng = np.random.default_rng(0)
+    rgb = rng.integers(0, 256, (40, 50, 3), dtype=np.uint8)
+    p = tmp_path / 'x.png'
+    Image.fromarray(rgb).save(p)
+    before, after, change = Loader(str(p), start=[5, 6], size=[10, 12], integrated=True)()
+    assert np.array_equal(before, rgb[5:15, 6:18, 1])   # cv2 BGR channel 1 = G
+    assert np.array_equal(after, rgb[5:15, 6:18, 0])    # cv2 channel 2 = R
+    assert np.array_equal(change, rgb[5:15, 6:18, 2])   # cv2 channel 0 = B
+    g = rng.integers(0, 256, (30, 30), dtype=np.uint8)
+    Image.fromarray(g).save(tmp_path / 'g1.png')
+    Image.fromarray(g[::-1]).save(tmp_path / 'g2.png')
+    a, b = Loader([str(tmp_path / 'g1.png'), str(tmp_path / 'g2.png')], start=[1, 2], size=[8, 9],
+                  integrated=False)()
+    assert np.array_equal(a, g[1:9, 2:11]) and np.array_equal(b, g[::-1][1:9, 2:11])
