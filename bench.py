@@ -1,0 +1,243 @@
+"""Benchmark: correlation-volume G-voxels/s and ms per stereo pair (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], "C3"): a synthetic 1024x1024 stereo pair (input
+1156x1156, so ImageCutSolver's floor rule yields 8x8 tiles of S = 128 = "d"), window 5,
+the reference's full 8-level pyramid, backtracking, sub-pixel refinement, elevation
+cal_map and stitching -- i.e. ImageCutSolver(img1, img2, image_size=[128,128],
+stride=[128,128], window_size=5)() on the GPU.  One step = one pair; inputs are
+resident in HBM before the timed region.  V = 64 tiles x 128^4 = 17.18 G voxels/pair.
+
+Multi-GPU (torchrun, one process per GPU): every rank solves its own pairs (pairs are
+independent: weak scaling, no collective on the data path); timing is barrier +
+synchronize bracketed, max over ranks.
+
+Also reported: the roofline of the dominant kernel (dm_corr_level1), timed with HIP
+events on the launch stream, the HBM roofline of the standalone level-0 volume kernel
+(dm_corr_volume, 4 B/voxel), and the CPU oracle's rate on a bounded sample (rank 0, N=1).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
+from deepmatching_stereo_matching_amd import engine  # noqa: E402
+from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+I8_MFMA_PEAK_TOPS = 4600.0     # dense int8 MFMA (2x bf16 dense ~2.3 PF)
+F64_VALU_PEAK_TFLOPS = 78.6    # FP64 vector peak
+WS = 5
+S = 128
+GRID = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--tile', type=int, default=S)
+    ap.add_argument('--grid', type=int, default=GRID)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample-tiles', type=int, default=2)
+    ap.add_argument('--no-volume', action='store_true')
+    return ap.parse_args()
+
+
+class PairSolver:
+    """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
+    dominant kernel (dm_corr_level1)."""
+
+    def __init__(self, img1, img2, tile, grid):
+        self.dev = img1.device
+        self.tile = tile
+        self.n, self.origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
+        assert self.n == [grid, grid], self.n
+        self.batch = engine.TileBatch(img1, img2, self.origins, tile, tile, WS,
+                                      L.DM_TM_CCOEFF_NORMED, self.dev)
+        self.ev = []
+
+    def step(self, timed=False):
+        pyr = engine.DevicePyramid(self.batch, build=False)
+        pyr.compute_stats()
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        pyr.build()                        # dm_corr_level1 + dm_aggregate levels
+        if timed:
+            e1.record()
+            self.ev.append((e0, e1))
+        match = pyr.match(sub_pix=True)
+        dmap, score = engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
+                                    ['elevation'])
+        return dmap, score
+
+    def level1_ms(self):
+        return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
+
+
+def time_level1_only(solver, reps=3):
+    """Average duration of dm_corr_level1 alone (HIP events, same stream)."""
+    pyr = engine.DevicePyramid(solver.batch, build=False)
+    pyr.compute_stats()
+    b = solver.batch
+    P1 = (b.h0 // 2) * (b.w0 // 2)
+    l1 = torch.empty((b.T, P1, P1), dtype=torch.float64, device=b.device)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        L.check(pyr.lib.dm_corr_level1(b.ref(), L.ptr(pyr.stats), L.ptr(l1), L.stream_handle()))
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.mean(ts))
+
+
+def volume_roofline(dev, tile):
+    """HBM roofline of the standalone level-0 volume kernel (dm_corr_volume) on 8 tiles."""
+    a, b = stereo_pair(2 * tile + WS - 1, 4 * tile + WS - 1, seed=77, dx=2)
+    n, org = engine.cut_grid(a.shape, [tile, tile], [tile, tile], WS)
+    batch = engine.TileBatch(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), org,
+                             tile, tile, WS, L.DM_TM_CCOEFF_NORMED, dev)
+    pyr = engine.DevicePyramid(batch, build=False)
+    pyr.compute_stats()
+    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=dev)
+    ts = []
+    for i in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        L.check(pyr.lib.dm_corr_volume(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
+        e1.record()
+        torch.cuda.synchronize()
+        if i:
+            ts.append(e0.elapsed_time(e1))
+    ms = float(np.mean(ts))
+    voxels = batch.T * batch.P * batch.P
+    gbs = 4.0 * voxels / (ms * 1e-3) / 1e9
+    del vol
+    return {'kernel': 'dm_corr_volume (k_minmax + k_volume)', 'tiles': batch.T, 'tile': tile,
+            'ms': round(ms, 3), 'algorithmic_bytes_per_voxel': 4, 'achieved': round(gbs, 1),
+            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def cpu_baseline(tiles, tile):
+    """The CPU oracle (port of the reference pipeline, OpenMP) on `tiles` tiles of the same
+    workload: corr_l0 + pyramid (libm pow) + matching + sub-pixel."""
+    from oracle import oracle as O
+    a, b = stereo_pair(tile + WS - 1, tiles * tile + WS - 1, seed=1000, dx=2)
+    O.set_pow_mode('libm')
+    t0 = time.perf_counter()
+    for k in range(tiles):
+        c0 = k * tile
+        l0 = O.corr_l0(a[:, c0:c0 + tile + WS - 1], b[:, c0:c0 + tile + WS - 1], WS)
+        levels, _, _ = O.pyramid(l0)
+        O.match(levels, sub_pix=True)
+        del l0, levels
+    dt = time.perf_counter() - t0
+    vox = tiles * float(tile) ** 4
+    cores = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+    return {'value': round(vox / dt / 1e9, 5), 'unit': 'Gvox/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d tiles of S=%d (%.2f G voxels) of the same workload, oracle/dm_oracle.c '
+                      '(OpenMP), %.2f s' % (tiles, tile, vox / 1e9, dt)}
+
+
+def load_traffic(tile):
+    """HBM bytes per launch of dm_corr_level1 from the committed rocprofv3 PMC passes."""
+    path = os.path.join(REPO, 'profiles', 'pmc_level1.json')
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get('tile') == tile:
+            return d.get('hbm_bytes_per_launch')
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local if dist else 0)
+    torch.cuda.set_device(dev)
+
+    tile, grid = args.tile, args.grid
+    # ImageCutSolver's floor rule (image_cut_solver.py:62): floor((side - (tile+ws-1)) / tile)
+    # tiles per axis, so a grid x grid cut needs side = (grid+1)*tile + ws-1 (1156 for C3)
+    side = (grid + 1) * tile + WS - 1
+    a, b = stereo_pair(side, side, seed=1000 + rank, dx=2, max_disp=tile // 4, sinusoidal=True)
+    img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    solver = PairSolver(img1, img2, tile, grid)
+    voxels = solver.batch.T * float(tile) ** 4
+
+    for _ in range(args.warmup):
+        solver.step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solver.step(timed=True)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_step = elapsed / args.steps * 1e3
+    value = world * args.steps * voxels / elapsed / 1e9
+    l1_ms = solver.level1_ms()
+    if rank == 0:
+        # dominant kernel: MFMA-side algorithmic ops = 2*ws^2 integer MACs per voxel
+        ops = 2.0 * WS * WS * voxels
+        achieved = ops / (l1_ms * 1e-3) / 1e12
+        traffic = load_traffic(tile)
+        roof = {'kernel': 'dm_corr_level1', 'bound': 'mfma', 'ms': round(l1_ms, 3),
+                'achieved': round(achieved, 2), 'peak': I8_MFMA_PEAK_TOPS, 'unit': 'TFLOP/s',
+                'frac': round(achieved / I8_MFMA_PEAK_TOPS, 5), 'traffic': traffic,
+                'algorithmic': '2*ws^2 = %d int ops per voxel x %d voxels per launch'
+                               % (2 * WS * WS, int(voxels))}
+        rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
+               'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world, 'steps': args.steps,
+               'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
+               'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
+               'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
+               'config': {'workload': 'C3: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
+                                      '+ sub-pixel + cal_map + stitch'
+                                      % (grid * tile, grid * tile, grid, grid, tile, WS),
+                          'tile': tile, 'tiles_per_pair': grid * grid, 'window_size': WS,
+                          'pairs_per_gpu_per_step': 1, 'parallelism': 'pairs sharded %d-way' % world},
+               'roofline': roof}
+        if not args.no_volume:
+            rec['volume_kernel_roofline'] = volume_roofline(dev, tile)
+        if world == 1 and not args.no_cpu_baseline:
+            rec['cpu_baseline'] = cpu_baseline(args.cpu_sample_tiles, tile)
+        print(json.dumps(rec))
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
