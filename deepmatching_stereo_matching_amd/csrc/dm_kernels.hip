@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -127,6 +128,8 @@ __device__ double l0_value(const Geo &g, const Stats &s, int t, int p0, int p1, 
     const float r = r_of_y(y_of_num(num, s.bQ[oq]), s.aP[op], g.method);
     return pow14((double)norm_x(r, s.rmn[op], s.rmx[op]));
 }
+
+#include "dm_mfma.h"
 
 // ------------------------------------------------------------------------------------
 // K2 (generic): one workgroup per level-1 cell (= 2x2 block of patches p).  For each
@@ -592,6 +595,18 @@ static Geo make_geo(const dm_tiles *b)
     return g;
 }
 
+static inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+static size_t base_stats_bytes(const dm_tiles *b) { return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0; }
+
+static void mfma_views(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
+{
+    const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
+    char *base = (char *)d_stats + align256(base_stats_bytes(b));
+    *Bw = (dm_v4i *)base;
+    *QS = (int2 *)(base + (size_t)b->T * b->h0 * G * KS * 1024);
+}
+
 static inline unsigned nblk(size_t n, unsigned bs)
 {
     size_t b = (n + bs - 1) / bs;
@@ -623,7 +638,9 @@ const char *dm_last_error(void) { return g_err; }
 size_t dm_stats_bytes(const dm_tiles *b)
 {
     if (!b) return 0;
-    return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0;
+    size_t n = base_stats_bytes(b);
+    if (b->ws >= 1 && b->ws <= 15 && mfma_eligible(b)) n = align256(n) + mfma_extra_bytes(b);
+    return n;
 }
 
 int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
@@ -635,6 +652,15 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
     dim3 grid(nblk(P, 256), b->T);
     k_stats<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), stats_view(d_stats, b->T, P));
     HIP_TRY(hipGetLastError());
+    if (mfma_eligible(b)) { // MFMA-B-ordered windows + packed per-window stats for dm_corr_level1
+        const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const size_t n = (size_t)b->T * b->h0 * G * 32;
+        k_prep_windows<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
+        HIP_TRY(hipGetLastError());
+    }
     return DM_OK;
 }
 
@@ -646,10 +672,29 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     if ((b->h0 & 1) || (b->w0 & 1))
         return fail(DM_ERR_SHAPE, "could not broadcast: map sides %dx%d must be even (Correlation_map.py:96-103)", b->h0, b->w0);
     const int P = b->h0 * b->w0;
-    if (P > DM_GENERIC_MAX_P || k2_lds_bytes(b->h0, b->w0, b->ws) > 160 * 1024)
-        return fail(DM_ERR_UNSUPPORTED, "tile too large for the generic level-1 kernel (P=%d)", P);
     Stats s = stats_view(d_stats, b->T, P);
     hipStream_t st = (hipStream_t)stream;
+    const char *force = getenv("DM_LEVEL1");
+    if (mfma_eligible(b) && !(force && strcmp(force, "generic") == 0)) {
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const int KS = (b->ws * b->ws + 31) / 32, G = b->w0 / 32;
+        const int waves = b->T * (b->h0 / 4) * (b->w0 / 8);
+        const unsigned grid = (unsigned)((waves + MF_WAVES - 1) / MF_WAVES);
+        const Geo gg = make_geo(b);
+#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mfma<KS_, G_><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
+        DM_MF(1, 2) DM_MF(1, 4) DM_MF(1, 8)
+        DM_MF(2, 2) DM_MF(2, 4) DM_MF(2, 8)
+        DM_MF(3, 2) DM_MF(3, 4) DM_MF(3, 8)
+        DM_MF(4, 2) DM_MF(4, 4) DM_MF(4, 8)
+        DM_MF(6, 2) DM_MF(6, 4) DM_MF(6, 8)
+        DM_MF(8, 2) DM_MF(8, 4) DM_MF(8, 8)
+#undef DM_MF
+        return fail(DM_ERR_UNSUPPORTED, "no MFMA instance for KS=%d G=%d", KS, G);
+    }
+    if (P > DM_GENERIC_MAX_P || k2_lds_bytes(b->h0, b->w0, b->ws) > 160 * 1024)
+        return fail(DM_ERR_UNSUPPORTED, "tile too large for the generic level-1 kernel (P=%d)", P);
     switch (b->ws) {
     case 1: return launch_level1<1>(b, s, d_level1, st);
     case 3: return launch_level1<3>(b, s, d_level1, st);

@@ -211,3 +211,28 @@ def test_shape_errors_like_reference(mirror):
     assert co.iteration == 1 and co.N_map == 1
     with pytest.raises(IndexError):              # Matching._B reads co_map_list[-2]
         MT.Matching(co)()
+
+
+@pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (128, 128, 5), (16, 64, 3), (32, 128, 7),
+                                      (64, 64, 15), (128, 256, 5)])
+def test_mfma_kernel_equals_generic(h0, w0, ws, monkeypatch):
+    """The MFMA level-1 kernel and the generic one agree bit for bit (level 1 + min/max)."""
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=h0 + w0 + ws, dx=3)
+    org = [(0, 0), (4, 8), (2, 3)]
+    res = {}
+    for mode in ('mfma', 'generic'):
+        monkeypatch.setenv('DM_LEVEL1', mode)
+        if mode == 'generic' and h0 * w0 > 16384:
+            continue
+        pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5))
+        st = pyr.stats.view(torch.float32)[4 * 3 * h0 * w0:6 * 3 * h0 * w0].cpu().numpy()
+        res[mode] = (pyr.levels[1].cpu().numpy(), st, pyr.match().cpu().numpy())
+    if 'generic' in res:
+        for x, y in zip(res['mfma'], res['generic']):
+            _same(x, y)
+    else:  # too big for the generic kernel: check one tile against the oracle
+        O.set_pow_mode('pinned')
+        lv, _, _ = O.pyramid(O.corr_l0(a[:h0 + ws - 1, :w0 + ws - 1], b[:h0 + ws - 1, :w0 + ws - 1], ws))
+        _same(res['mfma'][0][0], lv[1].reshape(res['mfma'][0][0].shape))
