@@ -22,8 +22,35 @@
 
 __constant__ double c_pow_tab[DM_POW_NT * 3] = DM_POW_TAB_INIT;
 __constant__ double c_pow_g[10] = DM_POW_G_INIT;
+__constant__ double c_powf_c[DM_POWF_NT] = DM_POWF_C_INIT;
+__constant__ double c_powf_p[DM_POWF_NT * 2] = DM_POWF_P_INIT;
+__constant__ double c_powf_g[(1 - DM_POWF_EMIN) * 2] = DM_POWF_G_INIT;
 
-__device__ __forceinline__ double pow14(double x) { return dm_pow14(x, c_pow_tab, c_pow_g); }
+__device__ __forceinline__ double pow14(double x)
+{
+    if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, c_powf_c, c_powf_p, c_powf_g);
+    return dm_pow14_slow(x, c_pow_tab, c_pow_g);
+}
+
+// fast-path tables staged in LDS by the level-1 kernels
+struct PowLds {
+    double fc[DM_POWF_NT];
+    double fp[DM_POWF_NT * 2];
+    double fg[(1 - DM_POWF_EMIN) * 2];
+};
+
+__device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
+{
+    for (int i = tid; i < DM_POWF_NT; i += nthreads) t.fc[i] = c_powf_c[i];
+    for (int i = tid; i < DM_POWF_NT * 2; i += nthreads) t.fp[i] = c_powf_p[i];
+    for (int i = tid; i < (1 - DM_POWF_EMIN) * 2; i += nthreads) t.fg[i] = c_powf_g[i];
+}
+
+__device__ __forceinline__ double pow14_lds(double x, const PowLds &t)
+{
+    if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, t.fc, t.fp, t.fg);
+    return dm_pow14_slow(x, c_pow_tab, c_pow_g);
+}
 
 // ------------------------------------------------------------------------------------
 // geometry + workspace views
@@ -71,6 +98,28 @@ __device__ __forceinline__ float y_of_num(int num, float b) { return __fmul_rn((
 __device__ __forceinline__ float norm_x(float r, float mn, float mx)
 {
     return __fdiv_rn(__fsub_rn(r, mn), __fsub_rn(mx, mn));
+}
+
+// Same value as norm_x, for a fixed patch: Markstein's correction of q = a * RN(1/den) is the
+// correctly rounded a/den for normal operands (Handbook of FP arithmetic, Markstein's
+// theorem; 5.4e8 random pairs checked).  Reachable operands are never subnormal: |r| is
+// 0 or >= ~1e-9 (f32(num) is an integer, a_p, b_q >= ~3e-5), so a = r - mn is 0 or
+// >= ~1e-16 and den is 0 or >= ~1e-16; den == 0 (constant map) gives NaN like 0/0.
+// rinv = __frcp_rn(den) is computed once per patch.
+__device__ __forceinline__ float norm_mk(float r, float mn, float den, float rinv)
+{
+    const float a = __fsub_rn(r, mn);
+    const float q = __fmul_rn(a, rinv);
+    const float e = __fmaf_rn(-q, den, a);
+    return __fmaf_rn(e, rinv, q);
+}
+
+// r_of_y with the clamp as one v_med3_f32 (r is never NaN)
+__device__ __forceinline__ float r_of_y_fast(float y, float a, int method)
+{
+    const float r = __fmul_rn(y, a);
+    if (method == DM_TM_CCOEFF) return r;
+    return a == 0.0f ? 1.0f : __builtin_amdgcn_fmed3f(r, -1.0f, 1.0f);
 }
 
 // ------------------------------------------------------------------------------------
@@ -599,9 +648,23 @@ static inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 static size_t base_stats_bytes(const dm_tiles *b) { return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0; }
 
+// level-1 kernel variant: 2 = MFMA 16x16x64 (default), 1 = MFMA 32x32x32, 0 = generic.
+// DM_LEVEL1=mf16|mf32|generic selects one for A/B runs; it must not change between
+// dm_corr_stats and dm_corr_level1 of one batch (the window layout differs).
+static int level1_variant(const dm_tiles *b)
+{
+    const char *f = getenv("DM_LEVEL1");
+    if (f && strcmp(f, "generic") == 0) return 0;
+    if (f && strcmp(f, "mf32") == 0) return mfma_eligible(b) ? 1 : 0;
+    if (mf16_eligible(b)) return 2;
+    return mfma_eligible(b) ? 1 : 0;
+}
+
 static void mfma_views(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
 {
-    const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
+    const bool v16 = level1_variant(b) == 2;
+    const int G = v16 ? b->w0 / 16 : b->w0 / 32;
+    const int KS = v16 ? (b->ws * b->ws + 63) / 64 : (b->ws * b->ws + 31) / 32;
     char *base = (char *)d_stats + align256(base_stats_bytes(b));
     *Bw = (dm_v4i *)base;
     *QS = (int2 *)(base + (size_t)b->T * b->h0 * G * KS * 1024);
@@ -638,9 +701,12 @@ const char *dm_last_error(void) { return g_err; }
 size_t dm_stats_bytes(const dm_tiles *b)
 {
     if (!b) return 0;
-    size_t n = base_stats_bytes(b);
-    if (b->ws >= 1 && b->ws <= 15 && mfma_eligible(b)) n = align256(n) + mfma_extra_bytes(b);
-    return n;
+    size_t n = base_stats_bytes(b), extra = 0;
+    if (b->ws >= 1 && b->ws <= 15 && b->T > 0 && b->h0 > 0 && b->w0 > 0) {
+        if (mfma_eligible(b)) extra = mfma_extra_bytes(b);
+        if (mf16_eligible(b) && mf16_extra_bytes(b) > extra) extra = mf16_extra_bytes(b);
+    }
+    return extra ? align256(n) + extra : n;
 }
 
 int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
@@ -652,13 +718,20 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
     dim3 grid(nblk(P, 256), b->T);
     k_stats<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), stats_view(d_stats, b->T, P));
     HIP_TRY(hipGetLastError());
-    if (mfma_eligible(b)) { // MFMA-B-ordered windows + packed per-window stats for dm_corr_level1
-        const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
+    const int var = level1_variant(b);
+    if (var) { // MFMA-B-ordered windows + packed per-window stats for dm_corr_level1
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
-        const size_t n = (size_t)b->T * b->h0 * G * 32;
-        k_prep_windows<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
+        if (var == 2) {
+            const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
+            const size_t n = (size_t)b->T * b->h0 * G * 16;
+            k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
+        } else {
+            const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
+            const size_t n = (size_t)b->T * b->h0 * G * 32;
+            k_prep_windows<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
+        }
         HIP_TRY(hipGetLastError());
     }
     return DM_OK;
@@ -674,8 +747,24 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     const int P = b->h0 * b->w0;
     Stats s = stats_view(d_stats, b->T, P);
     hipStream_t st = (hipStream_t)stream;
-    const char *force = getenv("DM_LEVEL1");
-    if (mfma_eligible(b) && !(force && strcmp(force, "generic") == 0)) {
+    const int var = level1_variant(b);
+    if (var == 2) {
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const int KS = (b->ws * b->ws + 63) / 64, G = b->w0 / 16;
+        const int waves = b->T * (b->h0 / 4) * (b->w0 / 4);
+        const unsigned grid = (unsigned)((waves + MF_WAVES - 1) / MF_WAVES);
+        const Geo gg = make_geo(b);
+#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mf16<KS_, G_><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
+        DM_MF(1, 2) DM_MF(1, 4) DM_MF(1, 8) DM_MF(1, 16)
+        DM_MF(2, 2) DM_MF(2, 4) DM_MF(2, 8) DM_MF(2, 16)
+        DM_MF(3, 2) DM_MF(3, 4) DM_MF(3, 8) DM_MF(3, 16)
+        DM_MF(4, 2) DM_MF(4, 4) DM_MF(4, 8) DM_MF(4, 16)
+#undef DM_MF
+        return fail(DM_ERR_UNSUPPORTED, "no MFMA16 instance for KS=%d G=%d", KS, G);
+    }
+    if (var == 1) {
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);

@@ -88,11 +88,9 @@ template <int KS, int G>
 __global__ __launch_bounds__(256) void k_level1_mfma(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                      const int2 *__restrict__ QS, double *L1)
 {
-    __shared__ double lds_tab[DM_POW_NT * 3];
-    __shared__ double lds_g[10];
+    __shared__ PowLds plds;
     const int tid = threadIdx.x;
-    for (int i = tid; i < DM_POW_NT * 3; i += 256) lds_tab[i] = c_pow_tab[i];
-    if (tid < 10) lds_g[tid] = c_pow_g[tid];
+    pow_lds_fill(plds, tid, 256);
     __syncthreads();
 
     const int lane = tid & 63, wave = tid >> 6;
@@ -219,12 +217,12 @@ __global__ __launch_bounds__(256) void k_level1_mfma(Geo g, Stats s, const dm_v4
                     const float R = fmaxf(Racc[m][r], Cm[m][r]);
                     Cprev[m][r] = Cm[m][r];
                     const float x = __fdiv_rn(__fsub_rn(r_of_y(R, ar[r], g.method), rmn[r]), den[r]);
-                    const double pv = dm_pow14((double)x, lds_tab, lds_g);
+                    const double pv = pow14_lds((double)x, plds);
                     sum = ch == 0 ? pv : sum + pv;
                 }
                 const int cl = 2 * sl + h;
                 const int cell = (I0 + (cl >> 2)) * w1 + (J0 + (cl & 3));
-                L1[((size_t)t * P1 + cell) * P1 + (size_t)u * w1 + v] = dm_pow14(sum / 4.0, lds_tab, lds_g);
+                L1[((size_t)t * P1 + cell) * P1 + (size_t)u * w1 + v] = pow14_lds(sum / 4.0, plds);
             }
         }
     }
@@ -239,4 +237,216 @@ static size_t mfma_extra_bytes(const dm_tiles *b)
 {
     const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
     return (size_t)b->T * b->h0 * G * KS * 1024 + (size_t)b->T * b->h0 * G * 32 * 8;
+}
+
+// ===================================================================================
+// 16x16x64 variant (default).  v_mfma_i32_16x16x64_i8: lane L holds A[row L&15][k = 64ks +
+// 16(L>>4) + j] and B[k][col L&15]; acc[reg] = C[row 4(L>>4) + reg][col L&15].
+// Rows: 16 patches = 4 level-1 cells (2x2 block = one level-2 cell) x 4 children, so lane
+// group L>>4 holds ONE cell and acc[reg] is child reg (ul, ur, ll, lr).  Columns: 16
+// windows of one image row, lane c = L&15 <-> q1 = G*c + tau, G = w0/16 tiles per row.
+// 4 accumulators per lane instead of 16 keep the per-lane pooling state small enough for
+// several waves per SIMD.
+// ===================================================================================
+
+// Bw16[t][q0][tau][ks][lane] (16 B): lane L = c + 16 hq holds taps k = 64 ks + 16 hq + j of
+// window (q0, G*c + tau);  QS16[t][q0][tau][c] = { -sum(I'), bits(b_q) }.
+__global__ void k_prep_windows16(Geo g, int G, int KS, dm_v4i *Bw, int2 *QS)
+{
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t total = (size_t)g.T * g.h0 * G * 16;
+    if (idx >= total) return;
+    const int c = (int)(idx % 16);
+    const int tau = (int)((idx / 16) % G);
+    const int q0 = (int)((idx / (16 * (size_t)G)) % g.h0);
+    const int t = (int)(idx / (16 * (size_t)G * g.h0));
+    const int q1 = G * c + tau;
+    const int ws = g.ws, n = ws * ws;
+    const uint8_t *base = g.img2 + (size_t)(g.org[2 * t] + q0) * g.pitch2 + g.org[2 * t + 1] + q1;
+    int s = 0, s2 = 0;
+    for (int u = 0; u < ws; ++u)
+        for (int v = 0; v < ws; ++v) {
+            const int b = (int)base[(size_t)u * g.pitch2 + v] - 128;
+            s += b; s2 += b * b;
+        }
+    const long long dI = (long long)n * s2 - (long long)s * s;
+    float bq;
+    if (g.method == DM_TM_CCOEFF) bq = 1.0f;
+    else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
+    QS[idx] = make_int2(-s, __float_as_int(bq));
+    const size_t tile = idx / 16; // (t, q0, tau)
+    for (int ks = 0; ks < KS; ++ks)
+        for (int hq = 0; hq < 4; ++hq) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * hq + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+            dm_v4i o;
+            o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
+            Bw[(tile * KS + ks) * 64 + c + 16 * hq] = o;
+        }
+}
+
+template <int KS>
+__device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__restrict__ Bt, int lane)
+{
+    dm_v4i acc = {};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[ks], Bt[ks * 64 + lane], acc, 0, 0, 0);
+    return acc;
+}
+
+__device__ __forceinline__ float shfl_prev16(float v, int lane)
+{
+    const float o = __shfl(v, lane - 1);
+    return (lane & 15) == 0 ? -INFINITY : o; // no q1 = -1 left of column 0
+}
+
+template <int KS, int G>
+__global__ __launch_bounds__(256, 4) void k_level1_mf16(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+                                                     const int2 *__restrict__ QS, double *L1)
+{
+    __shared__ PowLds plds;
+    const int tid = threadIdx.x;
+    pow_lds_fill(plds, tid, 256);
+    __syncthreads();
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int c = lane & 15, grp = lane >> 4;
+    const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
+    const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
+    const int nbj = w1 / 2, bpt = ((h0 / 2) / 2) * nbj; // 2x2-cell blocks per tile
+    const int gb = blockIdx.x * MF_WAVES + wave;
+    const int t = gb / bpt;
+    if (t >= g.T) return; // whole wave exits (no block-level sync below)
+    const int I0 = 2 * ((gb % bpt) / nbj), J0 = 2 * ((gb % bpt) % nbj);
+    const size_t tb = (size_t)t * P;
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+
+    // A operand: patch row rho = c: cell rho>>2, child rho&3; taps k = 64 ks + 16 grp + j
+    dm_v4i A[KS];
+    {
+        const int cl = c >> 2, ch = c & 3;
+        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
+        }
+    }
+    // this lane's cell (grp) and its 4 children (acc[reg], reg = child)
+    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
+    int sTr[4], pidx[4];
+    float ar[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        pidx[r] = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+        sTr[r] = s.sT[tb + pidx[r]];
+        ar[r] = s.aP[tb + pidx[r]];
+    }
+    const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
+    const int2 *Qt = QS + (size_t)t * h0 * G * 16;
+
+    // ---- sweep 1: per-patch min / max of y ----
+    float mn[4], mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
+    for (int ti = 0; ti < h0 * G; ++ti) {
+        const dm_v4i acc = mfma16_tile<KS>(A, Bt + (size_t)ti * KS * 64, lane);
+        const int2 qs = Qt[ti * 16 + c];
+        const float b = __int_as_float(qs.y);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+            mn[r] = fminf(mn[r], y);
+            mx[r] = fmaxf(mx[r], y);
+        }
+    }
+    float rmn[4], den[4], rinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        for (int off = 1; off < 16; off <<= 1) {
+            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
+            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        rmn[r] = r_of_y(mn[r], ar[r], g.method);
+        const float rmx = r_of_y(mx[r], ar[r], g.method);
+        den[r] = __fsub_rn(rmx, rmn[r]);
+        rinv[r] = __frcp_rn(den[r]);
+        if (c == 0) { s.rmn[tb + pidx[r]] = rmn[r]; s.rmx[tb + pidx[r]] = rmx; }
+    }
+
+    // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 ----
+    constexpr int M = G / 2; // pooled columns per lane: v = M*c + m
+    float Racc[M][4], Cprev[M][4];
+    double *Lrow = L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1;
+    for (int q0 = 0; q0 < h0; ++q0) {
+        float Cm[M][4], prev[4], xlast[4];
+        const dm_v4i *Brow = Bt + (size_t)q0 * G * KS * 64;
+        const int2 *Qrow = Qt + (size_t)q0 * G * 16;
+#pragma unroll
+        for (int it = 0; it < G; ++it) {
+            const int tau = it == 0 ? G - 1 : it - 1; // last tile first: it feeds lane c+1
+            const dm_v4i acc = mfma16_tile<KS>(A, Brow + (size_t)tau * KS * 64, lane);
+            const int2 qs = Qrow[tau * 16 + c];
+            const float b = __int_as_float(qs.y);
+            float y[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+            if (it == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { xlast[r] = y[r]; prev[r] = shfl_prev16(y[r], lane); }
+            } else if ((tau & 1) == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Cm[tau / 2][r] = fmaxf(prev[r], y[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { Cm[tau / 2][r] = fmaxf(Cm[tau / 2][r], y[r]); prev[r] = y[r]; }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cm[M - 1][r] = fmaxf(Cm[M - 1][r], xlast[r]);
+        if ((q0 & 1) == 0) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Racc[m][r] = q0 == 0 ? Cm[m][r] : fmaxf(Cprev[m][r], Cm[m][r]);
+            continue;
+        }
+        const int u = q0 >> 1;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            double sum = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
+                const float R = fmaxf(Racc[m][r], Cm[m][r]);
+                Cprev[m][r] = Cm[m][r];
+                const float x = norm_mk(r_of_y_fast(R, ar[r], g.method), rmn[r], den[r], rinv[r]);
+                const double pv = pow14_lds((double)x, plds);
+                sum = r == 0 ? pv : sum + pv;
+            }
+            Lrow[(size_t)u * w1 + M * c + m] = pow14_lds(sum / 4.0, plds);
+        }
+    }
+}
+
+static bool mf16_eligible(const dm_tiles *b)
+{
+    return b->h0 % 4 == 0 && b->w0 % 32 == 0 && b->w0 <= 256 && b->ws <= 15;
+}
+
+static size_t mf16_extra_bytes(const dm_tiles *b)
+{
+    const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
+    return (size_t)b->T * b->h0 * G * KS * 1024 + (size_t)b->T * b->h0 * G * 16 * 8;
 }

@@ -116,14 +116,18 @@ int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
 static int g_pow_mode = 0;
 static const double POW_TAB[] = DM_POW_TAB_INIT;
 static const double POW_G[] = DM_POW_G_INIT;
+static const double POWF_C[] = DM_POWF_C_INIT;
+static const double POWF_P[] = DM_POWF_P_INIT;
+static const double POWF_G[] = DM_POWF_G_INIT;
+static const dm_pow_tabs POW_TABS = {POWF_C, POWF_P, POWF_G, POW_TAB, POW_G};
 
 void dmo_set_pow_mode(int mode) { g_pow_mode = mode; }
 
-double dmo_pow14(double x) { return dm_pow14(x, POW_TAB, POW_G); }
+double dmo_pow14(double x) { return dm_pow14(x, &POW_TABS); }
 
 static inline double rect(double x, double lam)
 {
-    return g_pow_mode == 1 ? dm_pow14(x, POW_TAB, POW_G) : pow(x, lam);
+    return g_pow_mode == 1 ? dm_pow14(x, &POW_TABS) : pow(x, lam);
 }
 
 void dmo_rectify_f32(const float *in, long n, double lam, double *out)
