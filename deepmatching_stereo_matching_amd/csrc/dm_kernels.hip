@@ -51,6 +51,33 @@ __device__ __forceinline__ double pow14_lds(double x, const PowLds &t)
     if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, t.fc, t.fp, t.fg);
     return dm_pow14_slow(x, c_pow_tab, c_pow_g);
 }
+// dm_pow14_fast with the 2^(yE) row index clamped, so ANY input reads in-bounds LDS.
+// Identical to dm_pow14_fast on [2^-255, 1]; callers send other inputs to dm_pow14_slow.
+__device__ __forceinline__ double pow14_fast_any(double x, const PowLds &t)
+{
+    const uint64_t b = dm_bits_f64(x);
+    const int E = (int)(b >> 52) - 1023;
+    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int i = (int)((b >> 43) & (DM_POWF_NT - 1));
+    const double r = fma(M, t.fc[i], -1.0);
+    double q = DM_POWF_B6;
+    q = fma(q, r, DM_POWF_B5);
+    q = fma(q, r, DM_POWF_B4);
+    q = fma(q, r, DM_POWF_B3);
+    q = fma(q, r, DM_POWF_B2);
+    q = fma(q, r, DM_POWF_B1);
+    q = q * r;
+    const double Phi = t.fp[2 * i], Plo = t.fp[2 * i + 1];
+    const double Blo = fma(Phi, q, Plo);
+    const int e = min(max(E - DM_POWF_EMIN, 0), -DM_POWF_EMIN);
+    const double Ghi = t.fg[2 * e], Glo = t.fg[2 * e + 1];
+    const double Zhi = Phi * Ghi;
+    double s = fma(Phi, Ghi, -Zhi);
+    s = fma(Phi, Glo, s);
+    s = fma(Blo, Ghi, s);
+    return Zhi + s;
+}
+
 
 // ------------------------------------------------------------------------------------
 // geometry + workspace views
@@ -648,23 +675,24 @@ static inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 static size_t base_stats_bytes(const dm_tiles *b) { return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0; }
 
-// level-1 kernel variant: 2 = MFMA 16x16x64 (default), 1 = MFMA 32x32x32, 0 = generic.
-// DM_LEVEL1=mf16|mf32|generic selects one for A/B runs; it must not change between
+// level-1 kernel variant: 2 = MFMA 16x16x64 (default where eligible), 0 = generic.
+// DM_LEVEL1=generic forces the generic kernel for A/B runs; it must not change between
 // dm_corr_stats and dm_corr_level1 of one batch (the window layout differs).
 static int level1_variant(const dm_tiles *b)
 {
     const char *f = getenv("DM_LEVEL1");
     if (f && strcmp(f, "generic") == 0) return 0;
-    if (f && strcmp(f, "mf32") == 0) return mfma_eligible(b) ? 1 : 0;
-    if (mf16_eligible(b)) return 2;
-    return mfma_eligible(b) ? 1 : 0;
+    if (!mf16_eligible(b)) return 0;
+    if (f && strcmp(f, "mf16") == 0) return 2;
+    return 3; // column-split k_level1_mfq
 }
+
+// waves per workgroup of k_level1_mfq: NW = min(4, G/2); column group width GW = G/NW
+static int mfq_nw(const dm_tiles *b) { return b->w0 / 16 / 2 < 4 ? b->w0 / 16 / 2 : 4; }
 
 static void mfma_views(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
 {
-    const bool v16 = level1_variant(b) == 2;
-    const int G = v16 ? b->w0 / 16 : b->w0 / 32;
-    const int KS = v16 ? (b->ws * b->ws + 63) / 64 : (b->ws * b->ws + 31) / 32;
+    const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
     char *base = (char *)d_stats + align256(base_stats_bytes(b));
     *Bw = (dm_v4i *)base;
     *QS = (int2 *)(base + (size_t)b->T * b->h0 * G * KS * 1024);
@@ -702,10 +730,8 @@ size_t dm_stats_bytes(const dm_tiles *b)
 {
     if (!b) return 0;
     size_t n = base_stats_bytes(b), extra = 0;
-    if (b->ws >= 1 && b->ws <= 15 && b->T > 0 && b->h0 > 0 && b->w0 > 0) {
-        if (mfma_eligible(b)) extra = mfma_extra_bytes(b);
-        if (mf16_eligible(b) && mf16_extra_bytes(b) > extra) extra = mf16_extra_bytes(b);
-    }
+    if (b->ws >= 1 && b->ws <= 15 && b->T > 0 && b->h0 > 0 && b->w0 > 0 && mf16_eligible(b))
+        extra = mf16_extra_bytes(b);
     return extra ? align256(n) + extra : n;
 }
 
@@ -723,15 +749,10 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
-        if (var == 2) {
-            const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
-            const size_t n = (size_t)b->T * b->h0 * G * 16;
-            k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
-        } else {
-            const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
-            const size_t n = (size_t)b->T * b->h0 * G * 32;
-            k_prep_windows<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, KS, Bw, QS);
-        }
+        const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
+        const size_t n = (size_t)b->T * b->h0 * G * 16;
+        const int GW = var == 3 ? G / mfq_nw(b) : G;
+        k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
         HIP_TRY(hipGetLastError());
     }
     return DM_OK;
@@ -748,6 +769,27 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     Stats s = stats_view(d_stats, b->T, P);
     hipStream_t st = (hipStream_t)stream;
     const int var = level1_variant(b);
+    if (var == 3) {
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
+        const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
+        const Geo gg = make_geo(b);
+        const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 5 (default) or 6 waves/SIMD
+        if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] == '6') {
+            k_level1_mfq<1, 2, 4, 6><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, d_level1);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
+        DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
+        DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
+        DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4)
+        DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4)
+#undef DM_MQ
+        return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
+    }
     if (var == 2) {
         dm_v4i *Bw;
         int2 *QS;
@@ -756,31 +798,24 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
         const int waves = b->T * (b->h0 / 4) * (b->w0 / 4);
         const unsigned grid = (unsigned)((waves + MF_WAVES - 1) / MF_WAVES);
         const Geo gg = make_geo(b);
-#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mf16<KS_, G_><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
+        // A/B knobs (DM_MF16_MINW=3|4 waves per SIMD, DM_MF16_PF=0|1 tile prefetch) for the
+        // C3 shape; every other shape runs the default instance
+        const char *mw = getenv("DM_MF16_MINW"), *pf = getenv("DM_MF16_PF");
+        const int minw = (mw && mw[0] == '3') ? 3 : 4, pref = (pf && pf[0] == '1') ? 1 : 0;
+        if (KS == 1 && G == 8 && (minw != 4 || pref)) {
+            if (minw == 3 && pref) k_level1_mf16<1, 8, 3, true><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
+            else if (minw == 3) k_level1_mf16<1, 8, 3, false><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
+            else k_level1_mf16<1, 8, 4, true><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mf16<KS_, G_, 4, false><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
         DM_MF(1, 2) DM_MF(1, 4) DM_MF(1, 8) DM_MF(1, 16)
         DM_MF(2, 2) DM_MF(2, 4) DM_MF(2, 8) DM_MF(2, 16)
         DM_MF(3, 2) DM_MF(3, 4) DM_MF(3, 8) DM_MF(3, 16)
         DM_MF(4, 2) DM_MF(4, 4) DM_MF(4, 8) DM_MF(4, 16)
 #undef DM_MF
         return fail(DM_ERR_UNSUPPORTED, "no MFMA16 instance for KS=%d G=%d", KS, G);
-    }
-    if (var == 1) {
-        dm_v4i *Bw;
-        int2 *QS;
-        mfma_views(b, d_stats, &Bw, &QS);
-        const int KS = (b->ws * b->ws + 31) / 32, G = b->w0 / 32;
-        const int waves = b->T * (b->h0 / 4) * (b->w0 / 8);
-        const unsigned grid = (unsigned)((waves + MF_WAVES - 1) / MF_WAVES);
-        const Geo gg = make_geo(b);
-#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mfma<KS_, G_><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
-        DM_MF(1, 2) DM_MF(1, 4) DM_MF(1, 8)
-        DM_MF(2, 2) DM_MF(2, 4) DM_MF(2, 8)
-        DM_MF(3, 2) DM_MF(3, 4) DM_MF(3, 8)
-        DM_MF(4, 2) DM_MF(4, 4) DM_MF(4, 8)
-        DM_MF(6, 2) DM_MF(6, 4) DM_MF(6, 8)
-        DM_MF(8, 2) DM_MF(8, 4) DM_MF(8, 8)
-#undef DM_MF
-        return fail(DM_ERR_UNSUPPORTED, "no MFMA instance for KS=%d G=%d", KS, G);
     }
     if (P > DM_GENERIC_MAX_P || k2_lds_bytes(b->h0, b->w0, b->ws) > 160 * 1024)
         return fail(DM_ERR_UNSUPPORTED, "tile too large for the generic level-1 kernel (P=%d)", P);

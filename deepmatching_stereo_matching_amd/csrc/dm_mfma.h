@@ -1,243 +1,21 @@
-// dm_mfma.h -- MFMA (gfx950 v_mfma_i32_32x32x32_i8) path of the fused level-0 -> level-1
-// kernel.  Included by dm_kernels.hip after Geo/Stats/r_of_y/norm_x/pow14.
+// dm_mfma.h -- MFMA path (gfx950 v_mfma_i32_16x16x64_i8) of the fused level-0 -> level-1
+// kernel.  Included by dm_kernels.hip after Geo/Stats/r_of_y/norm_mk/pow14_fast_any.
 //
 // Reference semantics (misc/Correlation_map.py:69-159, misc/Feature_value.py:32-43): level 1
 // cell (I,J), position (u,v) = pow14( (R_ul + R_ur + R_ll + R_lr) / 4 ), R_c = MaxPool(3,2,1)
 // of the rectified min-max level-0 map of child patch c of the cell.
 //
-// GEMM view: num(p, q) = n * sum_k T'_k(p) I'_k(q) - sT(p) sI(q), k over the ws*ws taps.
-//   A (rows)    = 32 patches p of one wave: 8 level-1 cells x 4 children, row rho = 4*cell+child
-//   B (columns) = 32 windows q of one image row q0: lane c <-> q1 = G*c + tau (tile tau in [0,G),
-//                 G = w0/32), so MaxPool's column windows {2v-1, 2v, 2v+1} are in-lane except
-//                 one value per row from lane c-1.
-//   K           = taps, 32 per MFMA (KS = ceil(ws^2/32) MFMAs per tile), zero padded.
-// Output layout (32x32, dtype independent on gfx950): acc[reg] = C[row][col],
-//   col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
-// => a lane holds ONE window q and 16 patches = 4 cells x 4 children (child = reg & 3), so the
-//    4-child sum of the pyramid step is in-lane, in the reference's ul, ur, ll, lr order.
-//
+// GEMM view: num(p, q) = n * sum_k T'_k(p) I'_k(q) - sT(p) sI(q), k over the ws*ws taps (K
+// zero padded to 64 per MFMA, KS = ceil(ws^2/64) MFMAs per tile).
 // Sweep 1 computes y = f32(num) * b_q for every (p, q) and the per-patch min/max; sweep 2
 // recomputes y, pools on y (monotone, see dm_kernels.hip header), normalises and rectifies
 // only the pooled values, sums the children, rectifies, and stores level 1.
+// (A 32x32x32 variant, 8 cells per wave, ran at 1 wave/SIMD: 41 ms vs 25 ms per C3 pair.)
 #pragma once
 
 typedef int dm_v4i __attribute__((ext_vector_type(4)));
-typedef int dm_v16i __attribute__((ext_vector_type(16)));
 
 #define MF_WAVES 4
-
-// windows of img2 in MFMA-B order + per-window (-sI', b_q), for tiles with w0 % 64 == 0
-// Bw[t][q0][tau][ks][lane] (16 B): lane L = c + 32*h holds taps k = 32 ks + 16 h + j (j < 16)
-// of window (q0, G*c + tau); QS[t][q0][tau][c] = { -sum(I'), bits(b_q) }.
-__global__ void k_prep_windows(Geo g, int G, int KS, dm_v4i *Bw, int2 *QS)
-{
-    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t total = (size_t)g.T * g.h0 * G * 32;
-    if (idx >= total) return;
-    const int c = (int)(idx % 32);
-    const int tau = (int)((idx / 32) % G);
-    const int q0 = (int)((idx / (32 * (size_t)G)) % g.h0);
-    const int t = (int)(idx / (32 * (size_t)G * g.h0));
-    const int q1 = G * c + tau;
-    const int ws = g.ws, n = ws * ws;
-    const uint8_t *base = g.img2 + (size_t)(g.org[2 * t] + q0) * g.pitch2 + g.org[2 * t + 1] + q1;
-    int s = 0, s2 = 0;
-    for (int u = 0; u < ws; ++u)
-        for (int v = 0; v < ws; ++v) {
-            const int b = (int)base[(size_t)u * g.pitch2 + v] - 128;
-            s += b; s2 += b * b;
-        }
-    const long long dI = (long long)n * s2 - (long long)s * s;
-    float bq;
-    if (g.method == DM_TM_CCOEFF) bq = 1.0f;
-    else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
-    QS[idx] = make_int2(-s, __float_as_int(bq));
-    const size_t tile = idx / 32; // (t, q0, tau)
-    for (int ks = 0; ks < KS; ++ks)
-        for (int hh = 0; hh < 2; ++hh) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 32 * ks + 16 * hh + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            dm_v4i o;
-            o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
-            Bw[(tile * KS + ks) * 64 + c + 32 * hh] = o;
-        }
-}
-
-__device__ __forceinline__ float shfl_from_prev_lane(float v, int lane)
-{
-    // value of lane-1 within the same 32-lane half; lane c == 0 gets -inf (no q1 = -1)
-    const float o = __shfl(v, lane - 1);
-    return (lane & 31) == 0 ? -INFINITY : o;
-}
-
-template <int KS>
-__device__ __forceinline__ dm_v16i mfma_tile(const dm_v4i *A, const dm_v4i *__restrict__ Bt, int lane)
-{
-    dm_v16i acc = {};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[ks], Bt[ks * 64 + lane], acc, 0, 0, 0);
-    return acc;
-}
-
-template <int KS, int G>
-__global__ __launch_bounds__(256) void k_level1_mfma(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                     const int2 *__restrict__ QS, double *L1)
-{
-    __shared__ PowLds plds;
-    const int tid = threadIdx.x;
-    pow_lds_fill(plds, tid, 256);
-    __syncthreads();
-
-    const int lane = tid & 63, wave = tid >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
-    const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
-    const int nbj = w1 / 4, nbi = (h0 / 2) / 2, bpt = nbi * nbj; // 2x4-cell blocks
-    const int gb = blockIdx.x * MF_WAVES + wave;
-    const int t = gb / bpt;
-    if (t >= g.T) return; // whole wave exits (no block-level sync below)
-    const int bi = (gb % bpt) / nbj, bj = (gb % bpt) % nbj;
-    const int I0 = 2 * bi, J0 = 4 * bj;
-    const size_t tb = (size_t)t * P;
-    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-
-    // A operand: patch of p-row rho = c, taps k = 32 ks + 16 h + j
-    dm_v4i A[KS];
-    {
-        const int cl = c >> 2, ch = c & 3;
-        const int p0 = 2 * (I0 + (cl >> 2)) + (ch >> 1), p1 = 2 * (J0 + (cl & 3)) + (ch & 1);
-        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 32 * ks + 16 * h + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
-        }
-    }
-    // per-register patch constants: reg r <-> rho = (r&3) + 8(r>>2) + 4h: cell 2(r>>2)+h, child r&3
-    int sTr[16];
-    float ar[16];
-    int pidx[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int cl = 2 * (r >> 2) + h, ch = r & 3;
-        const int p0 = 2 * (I0 + (cl >> 2)) + (ch >> 1), p1 = 2 * (J0 + (cl & 3)) + (ch & 1);
-        pidx[r] = p0 * w0 + p1;
-        sTr[r] = s.sT[tb + pidx[r]];
-        ar[r] = s.aP[tb + pidx[r]];
-    }
-    const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
-    const int2 *Qt = QS + (size_t)t * h0 * G * 32;
-
-    // ---- sweep 1: per-patch min / max of y over all windows ----
-    float mn[16], mx[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
-    for (int ti = 0; ti < h0 * G; ++ti) {
-        const dm_v16i acc = mfma_tile<KS>(A, Bt + (size_t)ti * KS * 64, lane);
-        const int2 qs = Qt[ti * 32 + c];
-        const float b = __int_as_float(qs.y);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int num = __mul24(acc[r], n) + __mul24(sTr[r], qs.x);
-            const float y = __fmul_rn((float)num, b);
-            mn[r] = fminf(mn[r], y);
-            mx[r] = fmaxf(mx[r], y);
-        }
-    }
-    float rmn[16], den[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        for (int off = 1; off < 32; off <<= 1) {
-            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
-            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
-        }
-        rmn[r] = r_of_y(mn[r], ar[r], g.method);
-        const float rmx = r_of_y(mx[r], ar[r], g.method);
-        den[r] = __fsub_rn(rmx, rmn[r]);
-        if (c == 0) { s.rmn[tb + pidx[r]] = rmn[r]; s.rmx[tb + pidx[r]] = rmx; }
-    }
-
-    // ---- sweep 2: pool on y, normalise + rectify pooled values, children sum, level 1 ----
-    constexpr int M = G / 2; // pooled columns per lane per row: v = M*c + m
-    float Racc[M][16], Cprev[M][16];
-    for (int q0 = 0; q0 < h0; ++q0) {
-        float Cm[M][16], prev[16], xlast[16];
-        const dm_v4i *Brow = Bt + (size_t)q0 * G * KS * 64;
-        const int2 *Qrow = Qt + (size_t)q0 * G * 32;
-#pragma unroll
-        for (int it = 0; it < G; ++it) {
-            const int tau = it == 0 ? G - 1 : it - 1; // last tile first: its value feeds lane c+1
-            const dm_v16i acc = mfma_tile<KS>(A, Brow + (size_t)tau * KS * 64, lane);
-            const int2 qs = Qrow[tau * 32 + c];
-            const float b = __int_as_float(qs.y);
-            float y[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
-            if (it == 0) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) { xlast[r] = y[r]; prev[r] = shfl_from_prev_lane(y[r], lane); }
-            } else if ((tau & 1) == 0) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) Cm[tau / 2][r] = fmaxf(prev[r], y[r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) { Cm[tau / 2][r] = fmaxf(Cm[tau / 2][r], y[r]); prev[r] = y[r]; }
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) Cm[M - 1][r] = fmaxf(Cm[M - 1][r], xlast[r]);
-        if ((q0 & 1) == 0) {
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) Racc[m][r] = q0 == 0 ? Cm[m][r] : fmaxf(Cprev[m][r], Cm[m][r]);
-            continue;
-        }
-        const int u = q0 >> 1;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const int v = M * c + m;
-#pragma unroll
-            for (int sl = 0; sl < 4; ++sl) {
-                double sum = 0.0;
-#pragma unroll
-                for (int ch = 0; ch < 4; ++ch) { // ul, ur, ll, lr: left-to-right sum
-                    const int r = 4 * sl + ch;
-                    const float R = fmaxf(Racc[m][r], Cm[m][r]);
-                    Cprev[m][r] = Cm[m][r];
-                    const float x = __fdiv_rn(__fsub_rn(r_of_y(R, ar[r], g.method), rmn[r]), den[r]);
-                    const double pv = pow14_lds((double)x, plds);
-                    sum = ch == 0 ? pv : sum + pv;
-                }
-                const int cl = 2 * sl + h;
-                const int cell = (I0 + (cl >> 2)) * w1 + (J0 + (cl & 3));
-                L1[((size_t)t * P1 + cell) * P1 + (size_t)u * w1 + v] = pow14_lds(sum / 4.0, plds);
-            }
-        }
-    }
-}
-
-static bool mfma_eligible(const dm_tiles *b)
-{
-    return b->h0 % 4 == 0 && b->w0 % 64 == 0 && b->w0 <= 256 && b->ws <= 15;
-}
-
-static size_t mfma_extra_bytes(const dm_tiles *b)
-{
-    const int G = b->w0 / 32, KS = (b->ws * b->ws + 31) / 32;
-    return (size_t)b->T * b->h0 * G * KS * 1024 + (size_t)b->T * b->h0 * G * 32 * 8;
-}
 
 // ===================================================================================
 // 16x16x64 variant (default).  v_mfma_i32_16x16x64_i8: lane L holds A[row L&15][k = 64ks +
@@ -251,7 +29,10 @@ static size_t mfma_extra_bytes(const dm_tiles *b)
 
 // Bw16[t][q0][tau][ks][lane] (16 B): lane L = c + 16 hq holds taps k = 64 ks + 16 hq + j of
 // window (q0, G*c + tau);  QS16[t][q0][tau][c] = { -sum(I'), bits(b_q) }.
-__global__ void k_prep_windows16(Geo g, int G, int KS, dm_v4i *Bw, int2 *QS)
+// Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
+// lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
+// GW = G/NW: one group per wave of k_level1_mfq.
+__global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS)
 {
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t total = (size_t)g.T * g.h0 * G * 16;
@@ -260,7 +41,7 @@ __global__ void k_prep_windows16(Geo g, int G, int KS, dm_v4i *Bw, int2 *QS)
     const int tau = (int)((idx / 16) % G);
     const int q0 = (int)((idx / (16 * (size_t)G)) % g.h0);
     const int t = (int)(idx / (16 * (size_t)G * g.h0));
-    const int q1 = G * c + tau;
+    const int q1 = 16 * GW * (tau / GW) + GW * c + (tau % GW);
     const int ws = g.ws, n = ws * ws;
     const uint8_t *base = g.img2 + (size_t)(g.org[2 * t] + q0) * g.pitch2 + g.org[2 * t + 1] + q1;
     int s = 0, s2 = 0;
@@ -291,6 +72,22 @@ __global__ void k_prep_windows16(Geo g, int G, int KS, dm_v4i *Bw, int2 *QS)
 }
 
 template <int KS>
+__device__ __forceinline__ void load_frag(dm_v4i *f, const dm_v4i *__restrict__ Bt, int lane)
+{
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) f[ks] = Bt[ks * 64 + lane];
+}
+
+template <int KS>
+__device__ __forceinline__ dm_v4i mfma16_frag(const dm_v4i *A, const dm_v4i *Bf)
+{
+    dm_v4i acc = {};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[ks], Bf[ks], acc, 0, 0, 0);
+    return acc;
+}
+
+template <int KS>
 __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__restrict__ Bt, int lane)
 {
     dm_v4i acc = {};
@@ -305,8 +102,8 @@ __device__ __forceinline__ float shfl_prev16(float v, int lane)
     return (lane & 15) == 0 ? -INFINITY : o; // no q1 = -1 left of column 0
 }
 
-template <int KS, int G>
-__global__ __launch_bounds__(256, 4) void k_level1_mf16(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+template <int KS, int G, int MINW, bool PF>
+__global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                      const int2 *__restrict__ QS, double *L1)
 {
     __shared__ PowLds plds;
@@ -357,13 +154,32 @@ __global__ __launch_bounds__(256, 4) void k_level1_mf16(Geo g, Stats s, const dm
     const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
     const int2 *Qt = QS + (size_t)t * h0 * G * 16;
 
-    // ---- sweep 1: per-patch min / max of y ----
+    // ---- sweep 1: per-patch min / max of y (next tile's B / window stats prefetched) ----
     float mn[4], mx[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
-    for (int ti = 0; ti < h0 * G; ++ti) {
-        const dm_v4i acc = mfma16_tile<KS>(A, Bt + (size_t)ti * KS * 64, lane);
-        const int2 qs = Qt[ti * 16 + c];
+    const int NT = h0 * G;
+    dm_v4i bn[KS];
+    int2 qn;
+    if constexpr (PF) {
+        load_frag<KS>(bn, Bt, lane);
+        qn = Qt[c];
+    }
+    for (int ti = 0; ti < NT; ++ti) {
+        dm_v4i bc[KS];
+        int2 qs;
+        if constexpr (PF) { // software prefetch of the next tile
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) bc[ks] = bn[ks];
+            qs = qn;
+            const int tn = ti + 1 < NT ? ti + 1 : ti;
+            load_frag<KS>(bn, Bt + (size_t)tn * KS * 64, lane);
+            qn = Qt[tn * 16 + c];
+        } else {
+            load_frag<KS>(bc, Bt + (size_t)ti * KS * 64, lane);
+            qs = Qt[ti * 16 + c];
+        }
+        const dm_v4i acc = mfma16_frag<KS>(A, bc);
         const float b = __int_as_float(qs.y);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -387,18 +203,34 @@ __global__ __launch_bounds__(256, 4) void k_level1_mf16(Geo g, Stats s, const dm
     }
 
     // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 ----
+    // tile order per row: tau = G-1 first (its value feeds lane c+1), then 0 .. G-2
     constexpr int M = G / 2; // pooled columns per lane: v = M*c + m
     float Racc[M][4], Cprev[M][4];
     double *Lrow = L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1;
+    if constexpr (PF) {
+        load_frag<KS>(bn, Bt + (size_t)(G - 1) * KS * 64, lane);
+        qn = Qt[(G - 1) * 16 + c];
+    }
     for (int q0 = 0; q0 < h0; ++q0) {
         float Cm[M][4], prev[4], xlast[4];
-        const dm_v4i *Brow = Bt + (size_t)q0 * G * KS * 64;
-        const int2 *Qrow = Qt + (size_t)q0 * G * 16;
+        const int q0n = q0 + 1 < h0 ? q0 + 1 : q0;
 #pragma unroll
         for (int it = 0; it < G; ++it) {
-            const int tau = it == 0 ? G - 1 : it - 1; // last tile first: it feeds lane c+1
-            const dm_v4i acc = mfma16_tile<KS>(A, Brow + (size_t)tau * KS * 64, lane);
-            const int2 qs = Qrow[tau * 16 + c];
+            const int tau = it == 0 ? G - 1 : it - 1;
+            dm_v4i bc[KS];
+            int2 qs;
+            if constexpr (PF) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) bc[ks] = bn[ks];
+                qs = qn;
+                const int tn = it + 1 < G ? q0 * G + it : q0n * G + G - 1; // (row, tau) of the next tile
+                load_frag<KS>(bn, Bt + (size_t)tn * KS * 64, lane);
+                qn = Qt[tn * 16 + c];
+            } else {
+                load_frag<KS>(bc, Bt + (size_t)(q0 * G + tau) * KS * 64, lane);
+                qs = Qt[(q0 * G + tau) * 16 + c];
+            }
+            const dm_v4i acc = mfma16_frag<KS>(A, bc);
             const float b = __int_as_float(qs.y);
             float y[4];
 #pragma unroll
@@ -412,6 +244,178 @@ __global__ __launch_bounds__(256, 4) void k_level1_mf16(Geo g, Stats s, const dm
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { Cm[tau / 2][r] = fmaxf(Cm[tau / 2][r], y[r]); prev[r] = y[r]; }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cm[M - 1][r] = fmaxf(Cm[M - 1][r], xlast[r]);
+        if ((q0 & 1) == 0) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Racc[m][r] = q0 == 0 ? Cm[m][r] : fmaxf(Cprev[m][r], Cm[m][r]);
+            continue;
+        }
+        const int u = q0 >> 1;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            // (measured: computing the 4 fast pows branch-free and patching 0 / NaN afterwards
+            // needs more registers and ran 12-30 % slower than this per-child form)
+            double sum = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
+                const float R = fmaxf(Racc[m][r], Cm[m][r]);
+                Cprev[m][r] = Cm[m][r];
+                const float x = norm_mk(r_of_y_fast(R, ar[r], g.method), rmn[r], den[r], rinv[r]);
+                const double pv = pow14_lds((double)x, plds);
+                sum = r == 0 ? pv : sum + pv;
+            }
+            Lrow[(size_t)u * w1 + M * c + m] = pow14_lds(sum / 4.0, plds);
+        }
+    }
+}
+
+// ===================================================================================
+// Column-split variant (default).  One workgroup = NW waves = ONE 2x2 block of level-1
+// cells (16 patches, the same A operand in every wave); wave w sweeps only column group w
+// (16*GW window columns), so a lane pools GW/2 output columns instead of G/2 and the
+// per-lane state shrinks enough for more waves per SIMD.  Crossings: the per-patch
+// min/max is reduced over the waves through LDS once; MaxPool's left neighbour of column
+// group w (q1 = 16*GW*w - 1) comes from wave w-1 through LDS once per image row.
+// ===================================================================================
+template <int KS, int GW, int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+                                                        const int2 *__restrict__ QS, double *L1)
+{
+    __shared__ PowLds plds;
+    __shared__ float xch[2][NW][4][4]; // [row parity][wave][cell group][child]: y at q1 = 16*GW*(w+1)-1
+    __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
+    const int tid = threadIdx.x;
+    pow_lds_fill(plds, tid, 64 * NW);
+    __syncthreads();
+
+    constexpr int G = GW * NW;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int c = lane & 15, grp = lane >> 4;
+    const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
+    const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
+    const int nbj = w1 / 2, bpt = ((h0 / 2) / 2) * nbj; // 2x2-cell blocks per tile
+    const int t = blockIdx.x / bpt;                      // whole workgroup in range (grid exact)
+    const int I0 = 2 * ((blockIdx.x % bpt) / nbj), J0 = 2 * ((blockIdx.x % bpt) % nbj);
+    const size_t tb = (size_t)t * P;
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+
+    dm_v4i A[KS];
+    {
+        const int cl = c >> 2, ch = c & 3;
+        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
+        }
+    }
+    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
+    int sTr[4];
+    float ar[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+        sTr[r] = s.sT[tb + p];
+        ar[r] = s.aP[tb + p];
+    }
+    const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
+    const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
+
+    // ---- sweep 1: min / max of y over this wave's columns, then over the waves ----
+    float mn[4], mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
+    for (int q0 = 0; q0 < h0; ++q0) {
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            const size_t ti = (size_t)q0 * G + tw;
+            dm_v4i bc[KS];
+            load_frag<KS>(bc, Bt + ti * KS * 64, lane);
+            const int2 qs = Qt[ti * 16 + c];
+            const dm_v4i acc = mfma16_frag<KS>(A, bc);
+            const float b = __int_as_float(qs.y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+                mn[r] = fminf(mn[r], y);
+                mx[r] = fmaxf(mx[r], y);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        for (int off = 1; off < 16; off <<= 1) {
+            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
+            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        if (c == 0) { red[0][wave][4 * grp + r] = mn[r]; red[1][wave][4 * grp + r] = mx[r]; }
+    }
+    __syncthreads();
+    float rmn[4], den[4], rinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float a = red[0][0][4 * grp + r], b = red[1][0][4 * grp + r];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) { a = fminf(a, red[0][w][4 * grp + r]); b = fmaxf(b, red[1][w][4 * grp + r]); }
+        rmn[r] = r_of_y(a, ar[r], g.method);
+        const float rmx = r_of_y(b, ar[r], g.method);
+        den[r] = __fsub_rn(rmx, rmn[r]);
+        rinv[r] = __frcp_rn(den[r]);
+        if (wave == 0 && c == 0) {
+            const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+            s.rmn[tb + p] = rmn[r];
+            s.rmx[tb + p] = rmx;
+        }
+    }
+
+    // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 ----
+    constexpr int M = GW / 2; // pooled columns per lane: v = 8*GW*wave + M*c + m
+    float Racc[M][4], Cprev[M][4];
+    double *Lrow = L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wave;
+    for (int q0 = 0; q0 < h0; ++q0) {
+        float Cm[M][4], prev[4], xlast[4];
+#pragma unroll
+        for (int it = 0; it < GW; ++it) {
+            const int tw = it == 0 ? GW - 1 : it - 1; // last tile first: it feeds lane c+1
+            const size_t ti = (size_t)q0 * G + tw;
+            dm_v4i bc[KS];
+            load_frag<KS>(bc, Bt + ti * KS * 64, lane);
+            const int2 qs = Qt[ti * 16 + c];
+            const dm_v4i acc = mfma16_frag<KS>(A, bc);
+            const float b = __int_as_float(qs.y);
+            float y[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+            if (it == 0) {
+                if (c == 15) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xch[q0 & 1][wave][grp][r] = y[r];
+                }
+                __syncthreads(); // column group w's rightmost value reaches wave w+1
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    xlast[r] = y[r];
+                    const float o = __shfl(y[r], lane - 1);
+                    prev[r] = c != 0 ? o : (wave == 0 ? -INFINITY : xch[q0 & 1][wave - 1][grp][r]);
+                }
+            } else if ((tw & 1) == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Cm[tw / 2][r] = fmaxf(prev[r], y[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { Cm[tw / 2][r] = fmaxf(Cm[tw / 2][r], y[r]); prev[r] = y[r]; }
             }
         }
 #pragma unroll

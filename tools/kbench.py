@@ -36,7 +36,14 @@ def main():
     outs = {}
     for rnd in range(args.rounds + 1):
         for v in res:
-            os.environ['DM_LEVEL1'] = v
+            # "mf16+DM_MF16_MINW=4": kernel variant plus extra environment settings
+            parts = v.split('+')
+            os.environ['DM_LEVEL1'] = parts[0]
+            for kv in ('DM_MF16_MINW', 'DM_MF16_PF', 'DM_MFQ_MINW'):
+                os.environ.pop(kv, None)
+            for kv in parts[1:]:
+                k, val = kv.split('=')
+                os.environ[k] = val
             batch = engine.TileBatch(ia, ib, org, S, S, ws, L.DM_TM_CCOEFF_NORMED, dev)
             pyr = engine.DevicePyramid(batch, build=False).compute_stats()
             l1 = torch.empty((batch.T, P1, P1), dtype=torch.float64, device=dev)
