@@ -68,14 +68,11 @@ class PairSolver:
 
     def step(self, timed=False):
         pyr = engine.DevicePyramid(self.batch, build=False)
-        pyr.compute_stats()
+        ev = None
         if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        pyr.build()                        # dm_corr_level1 + dm_aggregate levels
-        if timed:
-            e1.record()
-            self.ev.append((e0, e1))
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev.append(ev)
+        pyr.build(events=ev)               # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
         match = pyr.match(sub_pix=True)
         dmap, score = engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                                     ['elevation'])
@@ -83,24 +80,6 @@ class PairSolver:
 
     def level1_ms(self):
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
-
-
-def time_level1_only(solver, reps=3):
-    """Average duration of dm_corr_level1 alone (HIP events, same stream)."""
-    pyr = engine.DevicePyramid(solver.batch, build=False)
-    pyr.compute_stats()
-    b = solver.batch
-    P1 = (b.h0 // 2) * (b.w0 // 2)
-    l1 = torch.empty((b.T, P1, P1), dtype=torch.float64, device=b.device)
-    ts = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        L.check(pyr.lib.dm_corr_level1(b.ref(), L.ptr(pyr.stats), L.ptr(l1), L.stream_handle()))
-        e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    return float(np.mean(ts))
 
 
 def volume_roofline(dev, tile):

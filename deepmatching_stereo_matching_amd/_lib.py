@@ -49,6 +49,7 @@ SIGNATURES = {
     'dm_stats_bytes': ([_TP], ctypes.c_size_t),
     'dm_corr_stats': ([_TP, _P, _P], ctypes.c_int),
     'dm_corr_level1': ([_TP, _P, _P, _P], ctypes.c_int),
+    'dm_corr_level12': ([_TP, _P, _P, _P, _P], ctypes.c_int),
     'dm_corr_volume': ([_TP, _P, _P, _P], ctypes.c_int),
     'dm_rectify': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify64': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),

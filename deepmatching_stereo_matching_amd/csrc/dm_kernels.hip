@@ -205,6 +205,29 @@ __device__ double l0_value(const Geo &g, const Stats &s, int t, int p0, int p1, 
     return pow14((double)norm_x(r, s.rmn[op], s.rmx[op]));
 }
 
+// Level-1 value of cell (I, J) at (u, v), on demand: MaxPool(3,2,1) of the four children's
+// rectified level-0 maps, (ul+ur+ll+lr)/4, rectify -- the same expression as k_aggregate
+// (Correlation_map.py:89-130) evaluated on l0_value, for matching when the fused
+// level-1/level-2 kernel kept level 1 on chip.
+__device__ double l1_value(const Geo &g, const Stats &s, int t, int I, int J, int u, int v)
+{
+    double acc = 0.0;
+    for (int ch = 0; ch < 4; ++ch) {
+        const int p0 = 2 * I + (ch >> 1), p1 = 2 * J + (ch & 1);
+        double mx = -INFINITY;
+        for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+            if (a < 0 || a >= g.h0) continue;
+            for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                if (b < 0 || b >= g.w0) continue;
+                const double x = l0_value(g, s, t, p0, p1, a, b);
+                mx = (x > mx || isnan(x)) ? x : mx;
+            }
+        }
+        acc = ch == 0 ? mx : acc + mx;
+    }
+    return pow14(acc / 4.0);
+}
+
 #include "dm_mfma.h"
 
 // ------------------------------------------------------------------------------------
@@ -448,8 +471,8 @@ __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r
 }
 
 // one _B step (:98-139): parent map (h x w) -> child map (2h x 2w) on level L (materialised
-// when L != nullptr, else level 0 on demand); at level 0 optionally _sub_pix_cal (:177-209)
-__global__ void k_match_step(Geo g, Stats s, const double *L, int T, int h, int w,
+// when L != nullptr, else level lev = 0 or 1 on demand); at level 0 optionally _sub_pix_cal (:177-209)
+__global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, int h, int w,
                              const double *pmap, double *cmap)
 {
     const int hn = 2 * h, wn = 2 * w;
@@ -471,7 +494,8 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int T, int h, int 
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) {
                 const int r = pd0 - 1 + a, c = pd1 - 1 + b;
-                win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0 : l0_value(g, s, t, p0, p1, r, c);
+                win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0
+                                 : lev == 0 ? l0_value(g, s, t, p0, p1, r, c) : l1_value(g, s, t, p0, p1, r, c);
             }
     }
     near_pick(win, pd0, pd1, o);
@@ -720,6 +744,34 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
+template <bool L2F>
+static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, hipStream_t st)
+{
+    dm_v4i *Bw;
+    int2 *QS;
+    mfma_views(b, d_stats, &Bw, &QS);
+    const Stats s = stats_view(d_stats, b->T, b->h0 * b->w0);
+    const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
+    const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
+    const Geo gg = make_geo(b);
+    const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 4, 5 or 6 waves/SIMD
+    if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] >= '4' && mw[0] <= '6') {
+        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 2, 4, 6, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
+    // register budget: 5 waves/SIMD without the level-2 tail, 4 with it (5 spills there)
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, L2F ? 4 : 5, L2F><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
+    DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
+    DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4)
+    DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4)
+#undef DM_MQ
+    return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
+}
+
 extern "C" {
 
 int dm_abi_version(void) { return 100; }
@@ -769,27 +821,7 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     Stats s = stats_view(d_stats, b->T, P);
     hipStream_t st = (hipStream_t)stream;
     const int var = level1_variant(b);
-    if (var == 3) {
-        dm_v4i *Bw;
-        int2 *QS;
-        mfma_views(b, d_stats, &Bw, &QS);
-        const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
-        const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
-        const Geo gg = make_geo(b);
-        const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 5 (default) or 6 waves/SIMD
-        if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] == '6') {
-            k_level1_mfq<1, 2, 4, 6><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, d_level1);
-            HIP_TRY(hipGetLastError());
-            return DM_OK;
-        }
-#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
-        DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
-        DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
-        DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4)
-        DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4)
-#undef DM_MQ
-        return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
-    }
+    if (var == 3) return launch_mfq<false>(b, d_stats, d_level1, nullptr, st);
     if (var == 2) {
         dm_v4i *Bw;
         int2 *QS;
@@ -830,6 +862,17 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     case 15: return launch_level1<15>(b, s, d_level1, st);
     }
     return fail(DM_ERR_UNSUPPORTED, "window size %d", b->ws);
+}
+
+int dm_corr_level12(const dm_tiles *b, void *d_stats, double *d_level1, double *d_level2, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats || !d_level2) return fail(DM_ERR_ARG, "null workspace / output");
+    if (level1_variant(b) != 3)
+        return fail(DM_ERR_UNSUPPORTED, "fused level-1/level-2 kernel needs h0 %% 4 == 0, w0 %% 32 == 0, w0 <= 256, ws <= 15 (got %dx%d, ws %d)",
+                    b->h0, b->w0, b->ws);
+    return launch_mfq<true>(b, d_stats, d_level1, d_level2, (hipStream_t)stream);
 }
 
 int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
@@ -888,8 +931,9 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
     const int K = nlev - 1;
     if ((h0 >> K) << K != h0 || (w0 >> K) << K != w0)
         return fail(DM_ERR_SHAPE, "map sides %dx%d not divisible by 2^(nlev-1) (nlev=%d)", h0, w0, nlev);
-    for (int l = 1; l < nlev; ++l)
-        if (!d_levels[l]) return fail(DM_ERR_ARG, "null level pointer %d", l);
+    for (int l = 1; l < nlev; ++l) // level 1 may be on demand too (dm_corr_level12), below the top
+        if (!d_levels[l] && !(l == 1 && nlev >= 3 && !d_levels[0]))
+            return fail(DM_ERR_ARG, "null level pointer %d", l);
     if (filter_num > 0 && (filter_window < 1 || filter_window > 7))
         return fail(DM_ERR_UNSUPPORTED, "filter_window_size %d not in [1, 7]", filter_window);
     if (filter_mode != 0 && filter_mode != 1) return fail(DM_ERR_ARG, "invalid filtering mode %d", filter_mode);
@@ -926,7 +970,7 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
     if (rc) return rc;
     for (int l = K - 1; l >= 0; --l) {
         const size_t n = (size_t)T * (2 * h) * (2 * w);
-        k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], T, h, w, buf[cur], buf[cur ^ 1]);
+        k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
         HIP_TRY(hipGetLastError());
         cur ^= 1;
         h *= 2; w *= 2;

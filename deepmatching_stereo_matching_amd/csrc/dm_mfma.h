@@ -282,13 +282,17 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
 // min/max is reduced over the waves through LDS once; MaxPool's left neighbour of column
 // group w (q1 = 16*GW*w - 1) comes from wave w-1 through LDS once per image row.
 // ===================================================================================
-template <int KS, int GW, int NW, int MINW>
+__device__ __forceinline__ double nanmax_d(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
+
+// L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
+template <int KS, int GW, int NW, int MINW, bool L2F>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                        const int2 *__restrict__ QS, double *L1)
+                                                        const int2 *__restrict__ QS, double *L1, double *L2)
 {
     __shared__ PowLds plds;
     __shared__ float xch[2][NW][4][4]; // [row parity][wave][cell group][child]: y at q1 = 16*GW*(w+1)-1
     __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
+    __shared__ double xch2[2][NW][4];  // [row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
     __syncthreads();
@@ -380,10 +384,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
     }
 
-    // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 ----
-    constexpr int M = GW / 2; // pooled columns per lane: v = 8*GW*wave + M*c + m
+    // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 [-> level 2] ----
+    constexpr int M = GW / 2;                 // pooled columns per lane: v = 8*GW*wave + M*c + m
+    constexpr int M2 = M >= 2 ? M / 2 : 1;    // level-2 columns per lane (M == 1: even lanes)
     float Racc[M][4], Cprev[M][4];
-    double *Lrow = L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wave;
+    double Racc2[M2], Cprev2[M2];
+    double *Lrow = L1 ? L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wave : nullptr;
+    const int w2 = w0 / 4, P2 = (h0 / 4) * w2;
+    double *L2row = L2F ? L2 + ((size_t)t * P2 + (size_t)(I0 / 2) * w2 + J0 / 2) * P2 : nullptr;
     for (int q0 = 0; q0 < h0; ++q0) {
         float Cm[M][4], prev[4], xlast[4];
 #pragma unroll
@@ -428,6 +436,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             continue;
         }
         const int u = q0 >> 1;
+        double l1v[M];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             double sum = 0.0;
@@ -439,14 +448,52 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 const double pv = pow14_lds((double)x, plds);
                 sum = r == 0 ? pv : sum + pv;
             }
-            Lrow[(size_t)u * w1 + M * c + m] = pow14_lds(sum / 4.0, plds);
+            l1v[m] = pow14_lds(sum / 4.0, plds);
+            if (L1) Lrow[(size_t)u * w1 + M * c + m] = l1v[m];
+        }
+        if constexpr (L2F) {
+            // level 2 of this workgroup's cell: NaN-propagating MaxPool(3,2,1) of the four
+            // level-1 maps (torch semantics, misc/Correlation_map.py:101-103), sum of the four
+            // maps in ul, ur, ll, lr order (:109-122), /4, rectify.  Columns: left neighbour
+            // from lane c-1 or, for c == 0, from wave w-1 through LDS; rows: streaming over u.
+            if (c == 15) xch2[u & 1][wave][grp] = l1v[M - 1];
+            __syncthreads();
+            const double lft = __shfl(l1v[M - 1], lane - 1);
+            const double left = c != 0 ? lft : (wave == 0 ? -INFINITY : xch2[u & 1][wave - 1][grp]);
+            double Cq[M2];
+            if constexpr (M == 1) { // L2 column 4*GW*w + c/2 on even lanes
+                const double right = __shfl(l1v[0], lane + 1);
+                Cq[0] = nanmax_d(nanmax_d(left, l1v[0]), right);
+            } else {
+#pragma unroll
+                for (int j = 0; j < M2; ++j)
+                    Cq[j] = nanmax_d(nanmax_d(j == 0 ? left : l1v[2 * j - 1], l1v[2 * j]), l1v[2 * j + 1]);
+            }
+            if ((u & 1) == 0) {
+#pragma unroll
+                for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : nanmax_d(Cprev2[j], Cq[j]);
+            } else {
+                const int u2 = u >> 1;
+#pragma unroll
+                for (int j = 0; j < M2; ++j) {
+                    const double R2 = nanmax_d(Racc2[j], Cq[j]);
+                    Cprev2[j] = Cq[j];
+                    const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
+                                 s3 = __shfl(R2, c + 48);
+                    const double l2 = pow14_lds((((s0 + s1) + s2) + s3) / 4.0, plds);
+                    const bool valid = M == 1 ? (c & 1) == 0 : true;
+                    const int col = M == 1 ? 4 * GW * wave + c / 2 : 4 * GW * wave + M2 * c + j;
+                    if (grp == 0 && valid) L2row[(size_t)u2 * w2 + col] = l2;
+                }
+            }
         }
     }
 }
 
 static bool mf16_eligible(const dm_tiles *b)
 {
-    return b->h0 % 4 == 0 && b->w0 % 32 == 0 && b->w0 <= 256 && b->ws <= 15;
+    // w0 in {32, 64, 128, 256}: the instantiated column-group counts G = w0/16 = 2, 4, 8, 16
+    return b->h0 % 4 == 0 && b->w0 >= 32 && b->w0 <= 256 && (b->w0 & (b->w0 - 1)) == 0 && b->ws <= 15;
 }
 
 static size_t mf16_extra_bytes(const dm_tiles *b)

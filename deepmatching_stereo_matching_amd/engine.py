@@ -84,16 +84,22 @@ class TileBatch:
 class DevicePyramid:
     """co_map_list of a TileBatch, resident on the device.
 
-    levels[0] is not stored (the fused kernel never writes level 0; matching evaluates it
-    on demand); levels[l] for l >= 1 are float64 [T][Pl][Pl] tensors."""
+    levels[0] is never stored (the fused kernels do not write level 0; matching evaluates
+    it on demand).  With ``fuse_level2`` (default; env DM_FUSE_L2=0 turns it off) and a
+    shape the fused level-1/level-2 kernel supports, level 1 stays on chip as well
+    (levels[1] is None until ``level(1)`` asks for it); levels[l] for the others are
+    float64 [T][Pl][Pl] tensors."""
 
-    def __init__(self, batch, stream=None, build=True):
+    def __init__(self, batch, stream=None, build=True, fuse_level2=None):
         self.b = batch
         self.lib = L.load()
         self.nlev, self.N_map = pyramid_plan(batch.h0, batch.w0)
         self.stream = stream
         self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
                                  device=batch.device)
+        if fuse_level2 is None:
+            fuse_level2 = os.environ.get('DM_FUSE_L2', '1') != '0'
+        self.fuse_level2 = bool(fuse_level2)
         self.levels = [None]
         self._volume = None
         self._have_minmax = False
@@ -111,18 +117,43 @@ class DevicePyramid:
             self._have_stats = True
         return self
 
-    def build(self):
+    def _empty_level(self, k):
+        b = self.b
+        Pk = (b.h0 >> k) * (b.w0 >> k)
+        return torch.empty((b.T, Pk, Pk), dtype=torch.float64, device=b.device)
+
+    def _level1(self):
+        l1 = self._empty_level(1)
+        L.check(self.lib.dm_corr_level1(self.b.ref(), L.ptr(self.stats), L.ptr(l1), self._s()),
+                'dm_corr_level1')
+        self._have_minmax = True
+        return l1
+
+    def build(self, events=None):
+        """Levels >= 1.  ``events``: optional (start, end) torch.cuda.Event pair recorded
+        around the level-1 (or fused level-1/level-2) kernel on this pyramid's stream."""
         b, lib = self.b, self.lib
         self.compute_stats()
         if self.nlev > 1 and len(self.levels) == 1:
-            P1 = (b.h0 // 2) * (b.w0 // 2)
-            l1 = torch.empty((b.T, P1, P1), dtype=torch.float64, device=b.device)
-            L.check(lib.dm_corr_level1(b.ref(), L.ptr(self.stats), L.ptr(l1), self._s()),
-                    'dm_corr_level1')
-            self.levels.append(l1)
-            self._have_minmax = True
             h, w = b.h0 // 2, b.w0 // 2
-            for _ in range(2, self.nlev):
+            fused = False
+            st = self.stream if self.stream is not None else torch.cuda.current_stream()
+            if events:
+                events[0].record(st)
+            if self.fuse_level2 and self.nlev >= 3:
+                l2 = self._empty_level(2)
+                rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), None, L.ptr(l2), self._s())
+                if rc == L.DM_OK:
+                    self.levels += [None, l2]
+                    self._have_minmax = True
+                    h, w, fused = h // 2, w // 2, True
+                elif rc != L.DM_ERR_UNSUPPORTED:
+                    L.check(rc, 'dm_corr_level12')
+            if not fused:
+                self.levels.append(self._level1())
+            if events:
+                events[1].record(st)
+            for _ in range(len(self.levels), self.nlev):
                 P2 = (h // 2) * (w // 2)
                 nxt = torch.empty((b.T, P2, P2), dtype=torch.float64, device=b.device)
                 L.check(lib.dm_aggregate(L.ptr(self.levels[-1]), b.T, h, w, 1, L.ptr(nxt),
@@ -154,6 +185,8 @@ class DevicePyramid:
         if not 0 <= k < self.nlev:
             raise IndexError('list index out of range')
         if k > 0:
+            if self.levels[k] is None:   # level 1 kept on chip by dm_corr_level12
+                self.levels[k] = self._level1()
             return self.levels[k]
         v = self.volume()
         out = torch.empty(v.shape, dtype=torch.float64, device=v.device)
@@ -168,7 +201,8 @@ class DevicePyramid:
             self.volume()
         out = torch.empty((b.T, 3, b.h0, b.w0), dtype=torch.float64, device=b.device)
         scratch = torch.empty_like(out)
-        ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [t.data_ptr() for t in self.levels[1:]]))
+        ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [None if t is None else t.data_ptr()
+                                                          for t in self.levels[1:]]))
         fnum = int(filtering_num) if filtering else 0
         L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, self.nlev, b.T, b.h0, b.w0,
                                   int(bool(sub_pix)), int(filter_window_size), fnum,

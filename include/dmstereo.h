@@ -85,6 +85,13 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream);
  * (:89-130) of _multi_level_correlation_pyramid (:132-156).  Needs dm_corr_stats first. */
 int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *stream);
 
+/* dm_corr_level1 followed by the second _aggregation (Correlation_map.py:89-130, :148-153)
+ * in the same kernel: writes level 2 (float64 [T][P2][P2], P2 = (h0/4)*(w0/4)) and, when
+ * d_level1 is non-NULL, level 1 as well.  With d_level1 NULL level 1 never reaches HBM;
+ * dm_match then evaluates it on demand.  Needs h0 % 4 == 0, w0 in {32,64,128,256},
+ * ws <= 15 (DM_ERR_UNSUPPORTED otherwise: use dm_corr_level1 + dm_aggregate). */
+int dm_corr_level12(const dm_tiles *b, void *d_stats, double *d_level1, double *d_level2, void *stream);
+
 /* Materialise the level-0 min-max volume "co_map" (float32 [T][P][P]) and the per-patch
  * min/max.  Replaces _create_simple_initial_co_map (:69-87) for callers that read
  * co_map directly (bad_matching.py:62-70).  Needs dm_corr_stats first. */
@@ -107,7 +114,9 @@ int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t re
 /* Coarse-to-fine matching on a pyramid of nlev levels of T tiles with level-0 sides
  * h0 x w0.  d_levels is a HOST array of nlev device pointers to float64 rectified levels
  * (co_map_list).  d_levels[0] may be NULL: level 0 is then evaluated on demand from the
- * images and the statistics (b and d_stats required; b->T/h0/w0 must match).
+ * images and the statistics (b and d_stats required; b->T/h0/w0 must match).  When
+ * d_levels[0] is NULL and nlev >= 3, d_levels[1] may be NULL as well (level 1 on demand,
+ * for a pyramid built by dm_corr_level12 without level 1).
  * filter_num > 0 runs Matching._filter (:224-255; filter_mode 0 average, 1 median, window
  * filter_window <= 7, square maps only) after the top level and after each _B step while
  * the count lasts, as Matching._initial_move_map / _B do.

@@ -213,6 +213,54 @@ def test_shape_errors_like_reference(mirror):
         MT.Matching(co)()
 
 
+@pytest.mark.parametrize('h0,w0,ws', [(32, 32, 5), (64, 64, 5), (128, 128, 5), (16, 64, 3),
+                                      (32, 128, 7), (64, 64, 15), (128, 256, 5), (64, 128, 9)])
+def test_fused_level2_equals_aggregate(h0, w0, ws):
+    """dm_corr_level12 (level 2 fused into the level-1 kernel, level 1 optionally written)
+    equals dm_corr_level1 + dm_aggregate bit for bit; matching with level 1 evaluated on
+    demand equals matching on the materialised level 1."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=7 * h0 + w0 + ws, dx=3)
+    org = [(0, 0), (4, 8), (2, 3)]
+    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=False)
+    fused = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=True)
+    assert fused.levels[1] is None and ref.levels[1] is not None
+    for k in range(2, ref.nlev):
+        _same(fused.levels[k].cpu().numpy(), ref.levels[k].cpu().numpy())
+    _same(fused.match().cpu().numpy(), ref.match().cpu().numpy())
+    if h0 == w0:   # Matching._filter is square-only (Matching.py:235-236)
+        _same(fused.match(filtering=True).cpu().numpy(), ref.match(filtering=True).cpu().numpy())
+    # both outputs at once
+    l1 = torch.empty_like(ref.levels[1])
+    l2 = torch.empty_like(ref.levels[2])
+    lib = L.load()
+    L.check(lib.dm_corr_level12(fused.b.ref(), L.ptr(fused.stats), L.ptr(l1), L.ptr(l2),
+                                L.stream_handle()))
+    _same(l1.cpu().numpy(), ref.levels[1].cpu().numpy())
+    _same(l2.cpu().numpy(), ref.levels[2].cpu().numpy())
+    _same(fused.level(1).cpu().numpy(), ref.levels[1].cpu().numpy())
+
+
+def test_fused_level2_unsupported_shapes():
+    """Shapes outside the fused kernel's range report DM_ERR_UNSUPPORTED; the engine then
+    builds level 1 + dm_aggregate."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(60, 110, seed=3, dx=2)
+    batch = engine.TileBatch(a, b, [(0, 0)], 32, 96, 5, 5)   # w0 = 96: not a power of two
+    pyr = engine.DevicePyramid(batch, fuse_level2=True)
+    assert pyr.levels[1] is not None
+    l2 = torch.empty((1, 8 * 24, 8 * 24), dtype=torch.float64, device='cuda')
+    rc = L.load().dm_corr_level12(batch.ref(), L.ptr(pyr.stats), None, L.ptr(l2), L.stream_handle())
+    assert rc == L.DM_ERR_UNSUPPORTED
+    O.set_pow_mode('pinned')
+    lv, _, _ = O.pyramid(O.corr_l0(a[:36, :100], b[:36, :100], 5))
+    _same(pyr.levels[2][0].cpu().numpy(), lv[2].reshape(pyr.levels[2][0].shape))
+
+
 @pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (128, 128, 5), (16, 64, 3), (32, 128, 7),
                                       (64, 64, 15), (128, 256, 5)])
 def test_mfma_kernel_equals_generic(h0, w0, ws, monkeypatch):
@@ -228,7 +276,7 @@ def test_mfma_kernel_equals_generic(h0, w0, ws, monkeypatch):
             continue
         pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5))
         st = pyr.stats.view(torch.float32)[4 * 3 * h0 * w0:6 * 3 * h0 * w0].cpu().numpy()
-        res[mode] = (pyr.levels[1].cpu().numpy(), st, pyr.match().cpu().numpy())
+        res[mode] = (pyr.level(1).cpu().numpy(), st, pyr.match().cpu().numpy())
     if 'generic' in res:
         for x, y in zip(res['mfma'], res['generic']):
             _same(x, y)
