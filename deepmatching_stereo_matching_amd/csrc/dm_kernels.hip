@@ -28,37 +28,47 @@ __constant__ double c_powf_g[(1 - DM_POWF_EMIN) * 2] = DM_POWF_G_INIT;
 
 __device__ __forceinline__ double pow14(double x)
 {
-    if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, c_powf_c, c_powf_p, c_powf_g);
+    if (x >= DM_POWF_XMIN && x <= 1.0) return dm_pow14_fast(x, c_powf_c, c_powf_p, c_powf_g);
     return dm_pow14_slow(x, c_pow_tab, c_pow_g);
 }
 
-// fast-path tables staged in LDS by the level-1 kernels
+// Fast-path tables staged in LDS by the level-1 kernels (gathers with random rows: strides
+// of 8 and 16 B spread over the banks; one 32-B row per index conflicted 4x more, measured):
+//   fc[i], fp[i] = c_i, (1/c_i)^y hi, lo                   per mantissa index
+//   gz[k]   = 2^(yE) hi, lo for E = k - 1 + EMIN (k >= 1);  gz[0] = 0 (x == 0 -> +0)
+//   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127), else 0
+// Same constants and the same operation sequence as dm_pow14_fast, so every variant below
+// returns dm_pow14's value on its domain.
+#define DM_GZ_ROWS (2 - DM_POWF_EMIN)
 struct PowLds {
     double fc[DM_POWF_NT];
-    double fp[DM_POWF_NT * 2];
-    double fg[(1 - DM_POWF_EMIN) * 2];
+    double fp[DM_POWF_NT][2];
+    double gz[DM_GZ_ROWS][2];
+    double g32[256][2];
 };
 
 __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
 {
-    for (int i = tid; i < DM_POWF_NT; i += nthreads) t.fc[i] = c_powf_c[i];
-    for (int i = tid; i < DM_POWF_NT * 2; i += nthreads) t.fp[i] = c_powf_p[i];
-    for (int i = tid; i < (1 - DM_POWF_EMIN) * 2; i += nthreads) t.fg[i] = c_powf_g[i];
+    for (int i = tid; i < DM_POWF_NT; i += nthreads) {
+        t.fc[i] = c_powf_c[i];
+        t.fp[i][0] = c_powf_p[2 * i];
+        t.fp[i][1] = c_powf_p[2 * i + 1];
+    }
+    for (int k = tid; k < DM_GZ_ROWS; k += nthreads) {
+        t.gz[k][0] = k ? c_powf_g[2 * (k - 1)] : 0.0;
+        t.gz[k][1] = k ? c_powf_g[2 * (k - 1) + 1] : 0.0;
+    }
+    for (int b = tid; b < 256; b += nthreads) {
+        const int e = b - 127 - DM_POWF_EMIN; // row of c_powf_g
+        const bool in = b >= 1 && b <= 127 && e >= 0;
+        t.g32[b][0] = in ? c_powf_g[2 * e] : 0.0;
+        t.g32[b][1] = in ? c_powf_g[2 * e + 1] : 0.0;
+    }
 }
 
-__device__ __forceinline__ double pow14_lds(double x, const PowLds &t)
+// dm_pow14_fast's arithmetic on mantissa M in [1,2), table index i and 2^(yE) row G
+__device__ __forceinline__ double pow14_core(double M, int i, const double *G, const PowLds &t)
 {
-    if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, t.fc, t.fp, t.fg);
-    return dm_pow14_slow(x, c_pow_tab, c_pow_g);
-}
-// dm_pow14_fast with the 2^(yE) row index clamped, so ANY input reads in-bounds LDS.
-// Identical to dm_pow14_fast on [2^-255, 1]; callers send other inputs to dm_pow14_slow.
-__device__ __forceinline__ double pow14_fast_any(double x, const PowLds &t)
-{
-    const uint64_t b = dm_bits_f64(x);
-    const int E = (int)(b >> 52) - 1023;
-    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
-    const int i = (int)((b >> 43) & (DM_POWF_NT - 1));
     const double r = fma(M, t.fc[i], -1.0);
     double q = DM_POWF_B6;
     q = fma(q, r, DM_POWF_B5);
@@ -67,10 +77,9 @@ __device__ __forceinline__ double pow14_fast_any(double x, const PowLds &t)
     q = fma(q, r, DM_POWF_B2);
     q = fma(q, r, DM_POWF_B1);
     q = q * r;
-    const double Phi = t.fp[2 * i], Plo = t.fp[2 * i + 1];
+    const double Phi = t.fp[i][0], Plo = t.fp[i][1];
     const double Blo = fma(Phi, q, Plo);
-    const int e = min(max(E - DM_POWF_EMIN, 0), -DM_POWF_EMIN);
-    const double Ghi = t.fg[2 * e], Glo = t.fg[2 * e + 1];
+    const double Ghi = G[0], Glo = G[1];
     const double Zhi = Phi * Ghi;
     double s = fma(Phi, Ghi, -Zhi);
     s = fma(Phi, Glo, s);
@@ -78,6 +87,47 @@ __device__ __forceinline__ double pow14_fast_any(double x, const PowLds &t)
     return Zhi + s;
 }
 
+// float64 input.  Exact dm_pow14 on [2^EMIN, 1] and 0; other inputs read in-bounds rows and
+// return garbage (NaN: callers add a NaN term).
+__device__ __forceinline__ double pow14_zd(double x, const PowLds &t)
+{
+    const uint64_t b = dm_bits_f64(x);
+    const unsigned hi = (unsigned)(b >> 32);
+    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int i = (int)((hi >> 11) & (DM_POWF_NT - 1));
+    const int be = (int)((hi >> 20) & 0x7FF);
+    const int k = min(max(be - (1022 + DM_POWF_EMIN), 0), DM_GZ_ROWS - 1);
+    return pow14_core(M, i, t.gz[k], t);
+}
+
+// float32 input (widened exactly): exact dm_pow14((double)x) for x == 0 and for normal
+// x in [2^EMIN, 1] (f32 subnormals would need renormalising: callers never produce them).
+// NaN gives garbage (callers add a NaN term).  Fewer integer ops than pow14_zd: exponent,
+// index and mantissa come straight from the f32 bits.
+__device__ __forceinline__ double pow14_zf(float x, const PowLds &t)
+{
+    const unsigned u = __float_as_uint(x);
+    const double M = (double)__uint_as_float((u & 0x7FFFFFu) | 0x3F800000u);
+    const int i = (int)((u >> 14) & (DM_POWF_NT - 1));
+    const int be = (int)((u >> 23) & 0xFF);
+    return pow14_core(M, i, t.g32[be], t);
+}
+
+__device__ __forceinline__ double pow14_lds(double x, const PowLds &t)
+{
+    if (x >= DM_POWF_XMIN && x <= 1.0) return pow14_zd(x, t);
+    return dm_pow14_slow(x, c_pow_tab, c_pow_g);
+}
+
+// pow14 for the fused level-1/level-2 kernels, branch-free.  Their inputs are 0, NaN or in
+// [2^-297, 1]: x = f32 in [0, 1] gives x^1.4 >= 2^-208.6 (f32's least subnormal is 2^-149),
+// the /4 child sums of those are >= 2^-210.6, their powers >= 2^-294.9 and the level-2 sums
+// >= 2^-297 -- all inside the fast path's [2^DM_POWF_EMIN, 1], so this equals pow14 there.
+static_assert(DM_POWF_EMIN <= -297, "fast-path table must cover every level-1/level-2 input");
+__device__ __forceinline__ double pow14_k(double x, const PowLds &t)
+{
+    return pow14_zd(x, t) + (x - x); // 0 -> +0 (zero row), NaN -> NaN
+}
 
 // ------------------------------------------------------------------------------------
 // geometry + workspace views
@@ -744,6 +794,34 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
+template <bool L2F, bool YF>
+static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
+                        hipStream_t st)
+{
+    const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
+    const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
+    const Geo gg = make_geo(b);
+    const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 4, 5 or 6 waves/SIMD
+    if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] >= '4' && mw[0] <= '6') {
+        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 2, 4, 6, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
+    // register budget: 5 waves/SIMD without the level-2 tail, 4 with it (5 spills there)
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, L2F ? 4 : 5, L2F, YF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
+    if constexpr (!YF) {
+        DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
+        DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4)
+        DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4)
+    }
+#undef DM_MQ
+    return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
+}
+
+// packed-f32 y (YF) needs n <= 25 (see y_of_acc); DM_MFQ_YF=0 forces the integer path (A/B)
 template <bool L2F>
 static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, hipStream_t st)
 {
@@ -751,25 +829,9 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
     int2 *QS;
     mfma_views(b, d_stats, &Bw, &QS);
     const Stats s = stats_view(d_stats, b->T, b->h0 * b->w0);
-    const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
-    const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
-    const Geo gg = make_geo(b);
-    const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 4, 5 or 6 waves/SIMD
-    if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] >= '4' && mw[0] <= '6') {
-        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 2, 4, 6, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        HIP_TRY(hipGetLastError());
-        return DM_OK;
-    }
-    // register budget: 5 waves/SIMD without the level-2 tail, 4 with it (5 spills there)
-#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, L2F ? 4 : 5, L2F><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
-    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
-    DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
-    DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4)
-    DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4)
-#undef DM_MQ
-    return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
+    const char *yf = getenv("DM_MFQ_YF");
+    if (b->ws <= 5 && !(yf && yf[0] == '0')) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st);
+    return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st);
 }
 
 extern "C" {

@@ -96,6 +96,45 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
     return acc;
 }
 
+// y = f32(num) * b_q for the 4 patches (acc[r]) of one lane against its window (qs).
+// YF (n <= 25): acc was accumulated onto DM_YBIAS, so its bits read as the float
+// 1.5*2^23 + acc (exact for |acc| <= 128^2 n < 2^22); with sTf = f32(sum T') and
+// -sum(I') = qs.x, sT*sI is exact in f32 (|.| <= (128 n)^2 < 2^24) and
+// fma(acc, n, -sT sI) rounds the exact integer num once -- the same f32(num) as the
+// integer path, in packed-f32 instructions (2 voxels each).
+#define DM_YBIAS 0x4B400000
+typedef float dm_f2 __attribute__((ext_vector_type(2)));
+
+template <bool YF>
+__device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, const float *sTf, int2 qs, int n,
+                                         float *y)
+{
+    const float b = __int_as_float(qs.y);
+    if constexpr (YF) {
+        const float nf = (float)n, sI = (float)qs.x;
+        const dm_f2 bias = {12582912.0f, 12582912.0f};
+        const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])} - bias;
+        const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])} - bias;
+        const dm_f2 p01 = dm_f2{sTf[0], sTf[1]} * dm_f2{sI, sI};
+        const dm_f2 p23 = dm_f2{sTf[2], sTf[3]} * dm_f2{sI, sI};
+        const dm_f2 n01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, p01);
+        const dm_f2 n23 = __builtin_elementwise_fma(a23, dm_f2{nf, nf}, p23);
+        const dm_f2 y01 = n01 * dm_f2{b, b}, y23 = n23 * dm_f2{b, b};
+        y[0] = y01.x; y[1] = y01.y; y[2] = y23.x; y[3] = y23.y;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+    }
+}
+
+template <int KS>
+__device__ __forceinline__ dm_v4i mfma16_frag_c(const dm_v4i *A, const dm_v4i *Bf, dm_v4i acc)
+{
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[ks], Bf[ks], acc, 0, 0, 0);
+    return acc;
+}
+
 __device__ __forceinline__ float shfl_prev16(float v, int lane)
 {
     const float o = __shfl(v, lane - 1);
@@ -285,14 +324,16 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
 __device__ __forceinline__ double nanmax_d(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
 
 // L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
-template <int KS, int GW, int NW, int MINW, bool L2F>
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
     __shared__ PowLds plds;
-    __shared__ float xch[2][NW][4][4]; // [row parity][wave][cell group][child]: y at q1 = 16*GW*(w+1)-1
+    __shared__ float xch[2][2][NW][4][4]; // [pair parity][row][wave][cell group][child]: y at q1 = 16*GW*(w+1)-1
     __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
-    __shared__ double xch2[2][NW][4];  // [row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
+    __shared__ double xch2[2][NW][4];  // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
+    __shared__ float4 cst[4][6];       // [cell][field][child]: a_p, lo, hi, rmin, den, rinv
+    __shared__ double cnan[4];         // [cell]: NaN if a child's map is constant (den == 0), else 0
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
     __syncthreads();
@@ -327,36 +368,58 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     }
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
-    float ar[4];
+    float sTf[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
         sTr[r] = s.sT[tb + p];
-        ar[r] = s.aP[tb + p];
+        sTf[r] = (float)sTr[r];
     }
+    const int ab = YF ? DM_YBIAS : 0;
+    const dm_v4i acc0 = {ab, ab, ab, ab};
     const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
     const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
+
+    // one image row of this wave's column group: GW tiles of B fragments + window stats.
+    // Rows are software-pipelined in pairs: the next row's loads are in flight while the
+    // current one is computed (prefetch row index clamped into range; its data is unused).
+    struct RowFrag {
+        dm_v4i b[GW][KS];
+        int2 q[GW];
+    };
+    auto load_row = [&](RowFrag &f, int q0) {
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            const size_t ti = (size_t)q0 * G + tw;
+            load_frag<KS>(f.b[tw], Bt + ti * KS * 64, lane);
+            f.q[tw] = Qt[ti * 16 + c];
+        }
+    };
 
     // ---- sweep 1: min / max of y over this wave's columns, then over the waves ----
     float mn[4], mx[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
-    for (int q0 = 0; q0 < h0; ++q0) {
+    auto minmax_row = [&](const RowFrag &f) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const size_t ti = (size_t)q0 * G + tw;
-            dm_v4i bc[KS];
-            load_frag<KS>(bc, Bt + ti * KS * 64, lane);
-            const int2 qs = Qt[ti * 16 + c];
-            const dm_v4i acc = mfma16_frag<KS>(A, bc);
-            const float b = __int_as_float(qs.y);
+            const dm_v4i acc = mfma16_frag_c<KS>(A, f.b[tw], acc0);
+            float y[4];
+            y_of_acc<YF>(acc, sTr, sTf, f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
-                mn[r] = fminf(mn[r], y);
-                mx[r] = fmaxf(mx[r], y);
+                mn[r] = fminf(mn[r], y[r]);
+                mx[r] = fmaxf(mx[r], y[r]);
             }
         }
+    };
+    RowFrag fa, fb;
+    load_row(fa, 0);
+    for (int q0 = 0; q0 < h0; q0 += 2) { // h0 % 4 == 0
+        load_row(fb, q0 + 1);
+        minmax_row(fa);
+        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0); // the last prefetch is sweep 2's row 0
+        minmax_row(fb);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -367,126 +430,172 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         if (c == 0) { red[0][wave][4 * grp + r] = mn[r]; red[1][wave][4 * grp + r] = mx[r]; }
     }
     __syncthreads();
-    float rmn[4], den[4], rinv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    // per-patch normalisation constants {a_p, rmin, rmax - rmin, RN(1/(rmax - rmin))} of the
+    // 16 patches -> LDS (read back at each level-1 row instead of holding 16 VGPRs)
+    // r_of_y as one med3(y * a_p, lo, hi): NORMED [-1, 1] ([1, 1] for a constant patch,
+    // a_p = 0: OpenCV's 1), CCOEFF unclamped
+    if (wave == 0 && c < 4) {
+        const int r = c;
+        const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+        const float ap = s.aP[tb + p];
         float a = red[0][0][4 * grp + r], b = red[1][0][4 * grp + r];
 #pragma unroll
         for (int w = 1; w < NW; ++w) { a = fminf(a, red[0][w][4 * grp + r]); b = fmaxf(b, red[1][w][4 * grp + r]); }
-        rmn[r] = r_of_y(a, ar[r], g.method);
-        const float rmx = r_of_y(b, ar[r], g.method);
-        den[r] = __fsub_rn(rmx, rmn[r]);
-        rinv[r] = __frcp_rn(den[r]);
-        if (wave == 0 && c == 0) {
-            const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
-            s.rmn[tb + p] = rmn[r];
-            s.rmx[tb + p] = rmx;
-        }
+        const float rmn = r_of_y(a, ap, g.method), rmx = r_of_y(b, ap, g.method);
+        const float den = __fsub_rn(rmx, rmn);
+        const bool cc = g.method == DM_TM_CCOEFF;
+        float *f = (float *)&cst[grp][0];
+        f[0 * 4 + r] = ap;
+        f[1 * 4 + r] = cc ? -INFINITY : (ap == 0.0f ? 1.0f : -1.0f);
+        f[2 * 4 + r] = cc ? INFINITY : 1.0f;
+        f[3 * 4 + r] = rmn;
+        f[4 * 4 + r] = den;
+        f[5 * 4 + r] = __frcp_rn(den);
+        s.rmn[tb + p] = rmn;
+        s.rmx[tb + p] = rmx;
+        const bool flat = den == 0.0f;
+        const bool any = __shfl(flat, lane - c) || __shfl(flat, lane - c + 1) || __shfl(flat, lane - c + 2) ||
+                         __shfl(flat, lane - c + 3);
+        if (r == 0) cnan[grp] = any ? (double)NAN : 0.0;
     }
+    __syncthreads();
 
     // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 [-> level 2] ----
     constexpr int M = GW / 2;                 // pooled columns per lane: v = 8*GW*wave + M*c + m
     constexpr int M2 = M >= 2 ? M / 2 : 1;    // level-2 columns per lane (M == 1: even lanes)
-    float Racc[M][4], Cprev[M][4];
-    double Racc2[M2], Cprev2[M2];
+    float Cprev[M][4];
+    double Racc2[M2], Cprev2[M2], l1p[M];
     double *Lrow = L1 ? L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wave : nullptr;
     const int w2 = w0 / 4, P2 = (h0 / 4) * w2;
     double *L2row = L2F ? L2 + ((size_t)t * P2 + (size_t)(I0 / 2) * w2 + J0 / 2) * P2 : nullptr;
-    for (int q0 = 0; q0 < h0; ++q0) {
-        float Cm[M][4], prev[4], xlast[4];
+
+    // column MaxPool(3,2,1) of one row on y: Cm[m] over q1 = 2v, 2v+1 and (m >= 1) 2v-1;
+    // the left neighbour of m = 0 (lane c-1's last tile) comes back in prev (lane c == 0:
+    // from wave w-1 through LDS after the barrier), the row's last tile in last.
+    auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&prev)[4], float (&last)[4]) {
 #pragma unroll
-        for (int it = 0; it < GW; ++it) {
-            const int tw = it == 0 ? GW - 1 : it - 1; // last tile first: it feeds lane c+1
-            const size_t ti = (size_t)q0 * G + tw;
-            dm_v4i bc[KS];
-            load_frag<KS>(bc, Bt + ti * KS * 64, lane);
-            const int2 qs = Qt[ti * 16 + c];
-            const dm_v4i acc = mfma16_frag<KS>(A, bc);
-            const float b = __int_as_float(qs.y);
+        for (int tw = 0; tw < GW; ++tw) {
+            const dm_v4i acc = mfma16_frag_c<KS>(A, f.b[tw], acc0);
             float y[4];
+            y_of_acc<YF>(acc, sTr, sTf, f.q[tw], n, y);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
-            if (it == 0) {
-                if (c == 15) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) xch[q0 & 1][wave][grp][r] = y[r];
-                }
-                __syncthreads(); // column group w's rightmost value reaches wave w+1
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    xlast[r] = y[r];
-                    const float o = __shfl(y[r], lane - 1);
-                    prev[r] = c != 0 ? o : (wave == 0 ? -INFINITY : xch[q0 & 1][wave - 1][grp][r]);
-                }
-            } else if ((tw & 1) == 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Cm[tw / 2][r] = fmaxf(prev[r], y[r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { Cm[tw / 2][r] = fmaxf(Cm[tw / 2][r], y[r]); prev[r] = y[r]; }
+            for (int r = 0; r < 4; ++r) {
+                if ((tw & 1) == 0) Cm[tw / 2][r] = tw == 0 ? y[r] : fmaxf(last[r], y[r]);
+                else Cm[tw / 2][r] = fmaxf(Cm[tw / 2][r], y[r]);
+                last[r] = y[r];
             }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Cm[M - 1][r] = fmaxf(Cm[M - 1][r], xlast[r]);
-        if ((q0 & 1) == 0) {
+        for (int r = 0; r < 4; ++r) prev[r] = __shfl(last[r], lane - 1);
+    };
+
+    // level 2 of this workgroup's cell from level-1 row u (values l1p, lane c == 15's value
+    // of wave w-1 in xch2[u & 1]): NaN-propagating MaxPool(3,2,1) of the four level-1 maps
+    // (torch semantics, misc/Correlation_map.py:101-103), sum of the four maps in ul, ur, ll,
+    // lr order (:109-122), /4, rectify; rows stream over u.
+    auto level2_row = [&](int u, const double (&l1p)[M]) {
+        const double lft = __shfl(l1p[M - 1], lane - 1);
+        const double left = c != 0 ? lft : (wave == 0 ? -INFINITY : xch2[u & 1][wave - 1][grp]);
+        double Cq[M2];
+        if constexpr (M == 1) { // L2 column 4*GW*w + c/2 on even lanes
+            const double right = __shfl(l1p[0], lane + 1);
+            Cq[0] = nanmax_d(nanmax_d(left, l1p[0]), right);
+        } else {
 #pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Racc[m][r] = q0 == 0 ? Cm[m][r] : fmaxf(Cprev[m][r], Cm[m][r]);
-            continue;
+            for (int j = 0; j < M2; ++j)
+                Cq[j] = nanmax_d(nanmax_d(j == 0 ? left : l1p[2 * j - 1], l1p[2 * j]), l1p[2 * j + 1]);
         }
-        const int u = q0 >> 1;
-        double l1v[M];
+        if ((u & 1) == 0) {
+#pragma unroll
+            for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : nanmax_d(Cprev2[j], Cq[j]);
+        } else {
+            const int u2 = u >> 1;
+#pragma unroll
+            for (int j = 0; j < M2; ++j) {
+                const double R2 = nanmax_d(Racc2[j], Cq[j]);
+                Cprev2[j] = Cq[j];
+                const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
+                             s3 = __shfl(R2, c + 48);
+                const double l2 = pow14_k((((s0 + s1) + s2) + s3) / 4.0, plds);
+                const bool valid = M == 1 ? (c & 1) == 0 : true;
+                const int col = M == 1 ? 4 * GW * wave + c / 2 : 4 * GW * wave + M2 * c + j;
+                if (grp == 0 && valid) L2row[(size_t)u2 * w2 + col] = l2;
+            }
+        }
+    };
+
+    // rows in pairs (q0 even, q0 + 1 odd) = level-1 row u = q0 / 2; one barrier per pair
+    // publishes both rows' edge values and the previous pair's level-1 edge value
+    for (int q0 = 0; q0 < h0; q0 += 2) {
+        const int u = q0 >> 1, k = u & 1;
+        load_row(fb, q0 + 1);
+        float Ca[M][4], Cb[M][4], pa[4], pb[4], la[4], lb[4];
+        pool_cols(fa, Ca, pa, la);
+        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
+        pool_cols(fb, Cb, pb, lb);
+        if (c == 15) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { xch[k][0][wave][grp][r] = la[r]; xch[k][1][wave][grp][r] = lb[r]; }
+            if (L2F && u > 0) xch2[k ^ 1][wave][grp] = l1p[M - 1];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (c == 0) {
+                pa[r] = wave == 0 ? -INFINITY : xch[k][0][wave - 1][grp][r];
+                pb[r] = wave == 0 ? -INFINITY : xch[k][1][wave - 1][grp][r];
+            }
+            Ca[0][r] = fmaxf(Ca[0][r], pa[r]);
+            Cb[0][r] = fmaxf(Cb[0][r], pb[r]);
+        }
+        double l1q[M]; // level-1 row u - 1, consumed by level2_row below
+#pragma unroll
+        for (int m = 0; m < M; ++m) l1q[m] = l1p[m];
+        // row pooling: even row q0 opens level-1 row u, odd row q0 + 1 closes it
+        // a constant child map (den == 0) makes its values NaN (0/0): its pow14_zf is garbage,
+        // the cell's NaN term restores the reference's NaN in the sum and in level 1
+        const float4 kap = cst[grp][0], klo = cst[grp][1], khi = cst[grp][2], kmn = cst[grp][3],
+                     kden = cst[grp][4], kinv = cst[grp][5];
+        const double nanc = cnan[grp];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
+            float R[4], x[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float Ra = q0 == 0 ? Ca[m][r] : fmaxf(Cprev[m][r], Ca[m][r]);
+                R[r] = fmaxf(Ra, Cb[m][r]);
+                Cprev[m][r] = Cb[m][r];
+            }
+            // r = med3(R * a_p, lo, hi); x = (r - rmin) / den (Markstein, see norm_mk), packed
+            const dm_f2 ra = dm_f2{R[0], R[1]} * dm_f2{kap.x, kap.y}, rb = dm_f2{R[2], R[3]} * dm_f2{kap.z, kap.w};
+            const float r4[4] = {__builtin_amdgcn_fmed3f(ra.x, klo.x, khi.x), __builtin_amdgcn_fmed3f(ra.y, klo.y, khi.y),
+                                 __builtin_amdgcn_fmed3f(rb.x, klo.z, khi.z), __builtin_amdgcn_fmed3f(rb.y, klo.w, khi.w)};
+            const dm_f2 a01 = dm_f2{r4[0], r4[1]} - dm_f2{kmn.x, kmn.y}, a23 = dm_f2{r4[2], r4[3]} - dm_f2{kmn.z, kmn.w};
+            const dm_f2 i01 = {kinv.x, kinv.y}, i23 = {kinv.z, kinv.w};
+            const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
+            const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{kden.x, kden.y}, a01);
+            const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{kden.z, kden.w}, a23);
+            const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01), x23 = __builtin_elementwise_fma(e23, i23, q23);
+            x[0] = x01.x; x[1] = x01.y; x[2] = x23.x; x[3] = x23.y;
             double sum = 0.0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
-                const float R = fmaxf(Racc[m][r], Cm[m][r]);
-                Cprev[m][r] = Cm[m][r];
-                const float x = norm_mk(r_of_y_fast(R, ar[r], g.method), rmn[r], den[r], rinv[r]);
-                const double pv = pow14_lds((double)x, plds);
+                const double pv = pow14_zf(x[r], plds);
                 sum = r == 0 ? pv : sum + pv;
             }
-            l1v[m] = pow14_lds(sum / 4.0, plds);
-            if (L1) Lrow[(size_t)u * w1 + M * c + m] = l1v[m];
+            sum = sum + nanc;
+            l1p[m] = pow14_zd(sum / 4.0, plds) + nanc;
+            if (L1) Lrow[(size_t)u * w1 + M * c + m] = l1p[m];
         }
         if constexpr (L2F) {
-            // level 2 of this workgroup's cell: NaN-propagating MaxPool(3,2,1) of the four
-            // level-1 maps (torch semantics, misc/Correlation_map.py:101-103), sum of the four
-            // maps in ul, ur, ll, lr order (:109-122), /4, rectify.  Columns: left neighbour
-            // from lane c-1 or, for c == 0, from wave w-1 through LDS; rows: streaming over u.
-            if (c == 15) xch2[u & 1][wave][grp] = l1v[M - 1];
-            __syncthreads();
-            const double lft = __shfl(l1v[M - 1], lane - 1);
-            const double left = c != 0 ? lft : (wave == 0 ? -INFINITY : xch2[u & 1][wave - 1][grp]);
-            double Cq[M2];
-            if constexpr (M == 1) { // L2 column 4*GW*w + c/2 on even lanes
-                const double right = __shfl(l1v[0], lane + 1);
-                Cq[0] = nanmax_d(nanmax_d(left, l1v[0]), right);
-            } else {
-#pragma unroll
-                for (int j = 0; j < M2; ++j)
-                    Cq[j] = nanmax_d(nanmax_d(j == 0 ? left : l1v[2 * j - 1], l1v[2 * j]), l1v[2 * j + 1]);
-            }
-            if ((u & 1) == 0) {
-#pragma unroll
-                for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : nanmax_d(Cprev2[j], Cq[j]);
-            } else {
-                const int u2 = u >> 1;
-#pragma unroll
-                for (int j = 0; j < M2; ++j) {
-                    const double R2 = nanmax_d(Racc2[j], Cq[j]);
-                    Cprev2[j] = Cq[j];
-                    const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
-                                 s3 = __shfl(R2, c + 48);
-                    const double l2 = pow14_lds((((s0 + s1) + s2) + s3) / 4.0, plds);
-                    const bool valid = M == 1 ? (c & 1) == 0 : true;
-                    const int col = M == 1 ? 4 * GW * wave + c / 2 : 4 * GW * wave + M2 * c + j;
-                    if (grp == 0 && valid) L2row[(size_t)u2 * w2 + col] = l2;
-                }
-            }
+            if (u > 0) level2_row(u - 1, l1q);
         }
+    }
+    if constexpr (L2F) {
+        const int u = h0 / 2 - 1;
+        if (c == 15) xch2[u & 1][wave][grp] = l1p[M - 1];
+        __syncthreads();
+        level2_row(u, l1p);
     }
 }
 

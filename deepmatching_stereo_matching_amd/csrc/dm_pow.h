@@ -122,6 +122,6 @@ DM_HD static __attribute__((noinline)) double dm_pow14_slow(double x, const doub
 /* x ** 1.4 for the double y = 1.4 (0x3FF6666666666666) */
 DM_HD static inline double dm_pow14(double x, const dm_pow_tabs *t)
 {
-    if (x >= 0x1p-255 && x <= 1.0) return dm_pow14_fast(x, t->fc, t->fp, t->fg);
+    if (x >= DM_POWF_XMIN && x <= 1.0) return dm_pow14_fast(x, t->fc, t->fp, t->fg);
     return dm_pow14_slow(x, t->tab, t->g);
 }
