@@ -72,7 +72,7 @@ class PairSolver:
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev.append(ev)
-        pyr.build(events=ev)               # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
+        pyr.build(events=ev)               # stats, dm_corr_level1 [timed], dm_aggregate levels 2..
         match = pyr.match(sub_pix=True)
         dmap, score = engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                                     ['elevation'])

@@ -333,6 +333,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
     __shared__ double xch2[2][NW][4];  // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
     __shared__ float4 cst[4][6];       // [cell][field][child]: a_p, lo, hi, rmin, den, rinv
+    // LATE: the next even row's fragments are loaded after the level-1 emission instead of
+    // before it (12 fewer live VGPRs through the emission, less latency cover)
+    constexpr bool LATE = L2F;
+    constexpr int L2V = 4 * GW, L2B = 64 / L2V; // level-2 values per wave per row; rows per stash
+    __shared__ double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: pow inputs
     __shared__ double cnan[4];         // [cell]: NaN if a child's map is constant (den == 0), else 0
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
@@ -509,17 +514,28 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 #pragma unroll
             for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : nanmax_d(Cprev2[j], Cq[j]);
         } else {
-            const int u2 = u >> 1;
+            // the wave's 4*GW level-2 values of row u2 (cell sums on lanes of group 0) go to
+            // the LDS stash; every L2B rows one pow per lane rectifies them all
+            const int u2 = u >> 1, slot = u2 % L2B;
 #pragma unroll
             for (int j = 0; j < M2; ++j) {
                 const double R2 = nanmax_d(Racc2[j], Cq[j]);
                 Cprev2[j] = Cq[j];
                 const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
                              s3 = __shfl(R2, c + 48);
-                const double l2 = pow14_k((((s0 + s1) + s2) + s3) / 4.0, plds);
                 const bool valid = M == 1 ? (c & 1) == 0 : true;
-                const int col = M == 1 ? 4 * GW * wave + c / 2 : 4 * GW * wave + M2 * c + j;
-                if (grp == 0 && valid) L2row[(size_t)u2 * w2 + col] = l2;
+                const int col = M == 1 ? c / 2 : M2 * c + j;
+                if (grp == 0 && valid) stash[wave][slot * L2V + col] = (((s0 + s1) + s2) + s3) / 4.0;
+            }
+            if (slot == L2B - 1 || u2 == h0 / 4 - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < (slot + 1) * L2V) {
+                    const double l2 = pow14_k(stash[wave][lane], plds);
+                    L2row[(size_t)(u2 - slot + lane / L2V) * w2 + 4 * GW * wave + lane % L2V] = l2;
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
     };
@@ -531,7 +547,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         load_row(fb, q0 + 1);
         float Ca[M][4], Cb[M][4], pa[4], pb[4], la[4], lb[4];
         pool_cols(fa, Ca, pa, la);
-        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
+        if constexpr (!LATE) load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
         pool_cols(fb, Cb, pb, lb);
         if (c == 15) {
 #pragma unroll
@@ -590,6 +606,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         if constexpr (L2F) {
             if (u > 0) level2_row(u - 1, l1q);
         }
+        if constexpr (LATE) load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
     }
     if constexpr (L2F) {
         const int u = h0 / 2 - 1;

@@ -85,9 +85,11 @@ class DevicePyramid:
     """co_map_list of a TileBatch, resident on the device.
 
     levels[0] is never stored (the fused kernels do not write level 0; matching evaluates
-    it on demand).  With ``fuse_level2`` (default; env DM_FUSE_L2=0 turns it off) and a
-    shape the fused level-1/level-2 kernel supports, level 1 stays on chip as well
-    (levels[1] is None until ``level(1)`` asks for it); levels[l] for the others are
+    it on demand).  With ``fuse_level2`` (env DM_FUSE_L2=1) and a shape the fused
+    level-1/level-2 kernel supports, level 1 stays on chip as well (levels[1] is None until
+    ``level(1)`` asks for it).  Off by default: on the C3 workload the fused kernel's extra
+    register pressure (4 instead of 5 waves/SIMD) costs more (~1.1 ms/pair) than writing
+    level 1 and pooling it with dm_aggregate (~0.8 ms/pair).  levels[l] for the others are
     float64 [T][Pl][Pl] tensors."""
 
     def __init__(self, batch, stream=None, build=True, fuse_level2=None):
@@ -98,7 +100,7 @@ class DevicePyramid:
         self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
                                  device=batch.device)
         if fuse_level2 is None:
-            fuse_level2 = os.environ.get('DM_FUSE_L2', '1') != '0'
+            fuse_level2 = os.environ.get('DM_FUSE_L2', '0') == '1'
         self.fuse_level2 = bool(fuse_level2)
         self.levels = [None]
         self._volume = None
