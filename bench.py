@@ -12,8 +12,9 @@ independent: weak scaling, no collective on the data path); timing is barrier +
 synchronize bracketed, max over ranks.
 
 Also reported: the roofline of the dominant kernel (dm_corr_level1), timed with HIP
-events on the launch stream, the HBM roofline of the standalone level-0 volume kernel
-(dm_corr_volume, 4 B/voxel), and the CPU oracle's rate on a bounded sample (rank 0, N=1).
+events on the launch stream inside the timed steps, the HBM roofline of the level-0
+volume kernel (dm_corr_volume, 4 B/voxel written) on the same batch, and the CPU oracle's
+rate on a bounded sample (rank 0, N=1).
 """
 
 import argparse
@@ -33,8 +34,6 @@ from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-I8_MFMA_PEAK_TOPS = 4600.0     # dense int8 MFMA (2x bf16 dense ~2.3 PF)
-F64_VALU_PEAK_TFLOPS = 78.6    # FP64 vector peak
 WS = 5
 S = 128
 GRID = 8
@@ -82,17 +81,15 @@ class PairSolver:
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
 
 
-def volume_roofline(dev, tile):
-    """HBM roofline of the standalone level-0 volume kernel (dm_corr_volume) on 8 tiles."""
-    a, b = stereo_pair(2 * tile + WS - 1, 4 * tile + WS - 1, seed=77, dx=2)
-    n, org = engine.cut_grid(a.shape, [tile, tile], [tile, tile], WS)
-    batch = engine.TileBatch(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), org,
-                             tile, tile, WS, L.DM_TM_CCOEFF_NORMED, dev)
+def volume_roofline(solver, reps=3):
+    """HBM roofline of the level-0 volume kernel (dm_corr_volume: co_map, float32, written in
+    full) on the same C3 batch: 4 B per voxel written."""
+    batch = solver.batch
     pyr = engine.DevicePyramid(batch, build=False)
     pyr.compute_stats()
-    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=dev)
+    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=batch.device)
     ts = []
-    for i in range(4):
+    for i in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         L.check(pyr.lib.dm_corr_volume(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
@@ -103,10 +100,12 @@ def volume_roofline(dev, tile):
     ms = float(np.mean(ts))
     voxels = batch.T * batch.P * batch.P
     gbs = 4.0 * voxels / (ms * 1e-3) / 1e9
-    del vol
-    return {'kernel': 'dm_corr_volume (k_minmax + k_volume)', 'tiles': batch.T, 'tile': tile,
-            'ms': round(ms, 3), 'algorithmic_bytes_per_voxel': 4, 'achieved': round(gbs, 1),
-            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4)}
+    del vol, pyr
+    torch.cuda.empty_cache()
+    return {'kernel': 'dm_corr_volume (k_volume_mfq)', 'tiles': batch.T, 'tile': batch.h0,
+            'ms': round(ms, 3), 'algorithmic_bytes_per_voxel': 4, 'bound': 'hbm',
+            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(batch.h0, 'volume')}
 
 
 def cpu_baseline(tiles, tile):
@@ -130,9 +129,10 @@ def cpu_baseline(tiles, tile):
                       '(OpenMP), %.2f s' % (tiles, tile, vox / 1e9, dt)}
 
 
-def load_traffic(tile):
-    """HBM bytes per launch of dm_corr_level1 from the committed rocprofv3 PMC passes."""
-    path = os.path.join(REPO, 'profiles', 'pmc_level1.json')
+def load_traffic(tile, kernel='level1'):
+    """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) of a kernel from
+    the committed rocprofv3 PMC passes (profiles/pmc_<kernel>.json, tools/profile.sh)."""
+    path = os.path.join(REPO, 'profiles', 'pmc_%s.json' % kernel)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -188,15 +188,16 @@ def main():
     value = world * args.steps * voxels / elapsed / 1e9
     l1_ms = solver.level1_ms()
     if rank == 0:
-        # dominant kernel: MFMA-side algorithmic ops = 2*ws^2 integer MACs per voxel
-        ops = 2.0 * WS * WS * voxels
-        achieved = ops / (l1_ms * 1e-3) / 1e12
-        traffic = load_traffic(tile)
-        roof = {'kernel': 'dm_corr_level1', 'bound': 'mfma', 'ms': round(l1_ms, 3),
-                'achieved': round(achieved, 2), 'peak': I8_MFMA_PEAK_TOPS, 'unit': 'TFLOP/s',
-                'frac': round(achieved / I8_MFMA_PEAK_TOPS, 5), 'traffic': traffic,
-                'algorithmic': '2*ws^2 = %d int ops per voxel x %d voxels per launch'
-                               % (2 * WS * WS, int(voxels))}
+        # dominant kernel: the fused level-0 -> level-1 kernel.  Algorithmic bytes per
+        # 4 B per level-0 voxel (the volume a materialising L0 kernel
+        # writes); this kernel keeps level 0 on chip, so "achieved" is the HBM-equivalent
+        # rate and "traffic" (PMC) the bytes it really moves.
+        gbs = 4.0 * voxels / (l1_ms * 1e-3) / 1e9
+        roof = {'kernel': 'dm_corr_level1 (k_level1_mfq)', 'bound': 'hbm', 'ms': round(l1_ms, 3),
+                'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(tile),
+                'algorithmic': '4 B/voxel x %d voxels per launch (level 0 never leaves the chip)'
+                               % int(voxels)}
         rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
                'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
@@ -209,7 +210,7 @@ def main():
                           'pairs_per_gpu_per_step': 1, 'parallelism': 'pairs sharded %d-way' % world},
                'roofline': roof}
         if not args.no_volume:
-            rec['volume_kernel_roofline'] = volume_roofline(dev, tile)
+            rec['volume_kernel_roofline'] = volume_roofline(solver)
         if world == 1 and not args.no_cpu_baseline:
             rec['cpu_baseline'] = cpu_baseline(args.cpu_sample_tiles, tile)
         print(json.dumps(rec))

@@ -945,6 +945,24 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
     const int P = b->h0 * b->w0;
     Stats s = stats_view(d_stats, b->T, P);
     dim3 grid(P, b->T);
+    if (level1_variant(b) == 3) { // MFMA path (the column-group window layout of dm_corr_stats)
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const int KS = (b->ws * b->ws + 63) / 64, GW = b->w0 / 16 / mfq_nw(b);
+        const size_t waves = (size_t)b->T * (b->h0 / 4) * (b->w0 / 4);
+        const unsigned vgrid = (unsigned)((waves + 3) / 4);
+        const char *nt = getenv("DM_VOLUME_NT");
+        const bool ntst = !(nt && nt[0] == '0');
+        const bool yf = b->ws <= 5;
+        const Geo gg = make_geo(b);
+        hipStream_t st = (hipStream_t)stream;
+#define DM_VQ(KS_, GW_, YF_, NT_) if (KS == KS_ && GW == GW_ && yf == YF_ && ntst == NT_) { k_volume_mfq<KS_, GW_, YF_, NT_><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0); HIP_TRY(hipGetLastError()); return DM_OK; }
+        DM_VQ(1, 2, true, true) DM_VQ(1, 4, true, true) DM_VQ(1, 2, true, false) DM_VQ(1, 4, true, false)
+        DM_VQ(1, 2, false, true) DM_VQ(1, 4, false, true) DM_VQ(2, 2, false, true) DM_VQ(2, 4, false, true)
+        DM_VQ(3, 2, false, true) DM_VQ(3, 4, false, true) DM_VQ(4, 2, false, true) DM_VQ(4, 4, false, true)
+#undef DM_VQ
+    }
     k_minmax<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s);
     HIP_TRY(hipGetLastError());
     k_volume<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s, d_l0);

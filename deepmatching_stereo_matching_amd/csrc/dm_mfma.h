@@ -616,6 +616,155 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     }
 }
 
+// ===================================================================================
+// Level-0 volume ("co_map", misc/Correlation_map.py:69-87 + Feature_value.min_max), MFMA
+// path: one wave per 16 patches (a 2x2 block of level-1 cells, as k_level1_mfq), every wave
+// independent (no LDS, no barrier).  Sweep 1: min/max of y over all windows; sweep 2:
+// recompute y, r = med3(y a_p, lo, hi), x = (r - rmin)/den (Markstein), store float32.
+// Windows use the column-group layout of k_prep_windows16 (q1 = 16 GW g + GW c + tw), so
+// lane c's GW tiles of group g are GW consecutive floats: one GW-float vector store per
+// patch, a 16-lane group writing 64*GW/... = 16*GW*4 contiguous bytes of the patch's row.
+// ===================================================================================
+template <int KS, int GW, bool YF, bool NT>
+__global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+                                                    const int2 *__restrict__ QS, float *vol)
+{
+    const int lane = threadIdx.x & 63;
+    const int c = lane & 15, grp = lane >> 4;
+    const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
+    const int G = w0 / 16, NG = G / GW; // tiles per row, column groups per row
+    const int nbj = w0 / 4, bpt = (h0 / 4) * nbj;
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wid >= g.T * bpt) return; // whole wave
+    const int t = wid / bpt;
+    const int I0 = 2 * ((wid % bpt) / nbj), J0 = 2 * ((wid % bpt) % nbj);
+    const size_t tb = (size_t)t * P;
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+
+    dm_v4i A[KS];
+    {
+        const int cl = c >> 2, ch = c & 3;
+        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
+        }
+    }
+    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
+    int sTr[4], pr[4];
+    float sTf[4], ap[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        pr[r] = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+        sTr[r] = s.sT[tb + pr[r]];
+        sTf[r] = (float)sTr[r];
+        ap[r] = s.aP[tb + pr[r]];
+    }
+    const int ab = YF ? DM_YBIAS : 0;
+    const dm_v4i acc0 = {ab, ab, ab, ab};
+    const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
+    const int2 *Qt = QS + (size_t)t * h0 * G * 16;
+
+    // unit = (row q0, column group gg): GW tiles; double-buffered loads
+    struct Unit {
+        dm_v4i b[GW][KS];
+        int2 q[GW];
+    };
+    const int NU = h0 * NG;
+    auto load_unit = [&](Unit &f, int uidx) {
+        const int q0 = uidx / NG, gg = uidx % NG;
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            const size_t ti = (size_t)q0 * G + gg * GW + tw;
+            load_frag<KS>(f.b[tw], Bt + ti * KS * 64, lane);
+            f.q[tw] = Qt[ti * 16 + c];
+        }
+    };
+
+    float mn[4], mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
+    Unit fa, fb;
+    load_unit(fa, 0);
+    for (int ui = 0; ui < NU; ui += 2) { // NU even (h0 % 4 == 0)
+        load_unit(fb, ui + 1);
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
+        }
+        load_unit(fa, ui + 2 < NU ? ui + 2 : 0); // last prefetch = sweep 2's first unit
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
+        }
+    }
+    float lo[4], hi[4], rmn[4], den[4], rinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        for (int off = 1; off < 16; off <<= 1) {
+            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
+            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        rmn[r] = r_of_y(mn[r], ap[r], g.method);
+        const float rmx = r_of_y(mx[r], ap[r], g.method);
+        den[r] = __fsub_rn(rmx, rmn[r]);
+        rinv[r] = __frcp_rn(den[r]);
+        const bool cc = g.method == DM_TM_CCOEFF;
+        lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
+        hi[r] = cc ? INFINITY : 1.0f;
+        if (c == 0) {
+            s.rmn[tb + pr[r]] = rmn[r];
+            s.rmx[tb + pr[r]] = rmx;
+        }
+    }
+
+    typedef float fv __attribute__((ext_vector_type(GW)));
+    auto emit = [&](const Unit &f, int uidx) {
+        const int q0 = uidx / NG, gg = uidx % NG;
+        float xs[GW][4];
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);
+                xs[tw][r] = norm_mk(rr, rmn[r], den[r], rinv[r]);
+            }
+        }
+        const size_t qoff = (size_t)q0 * w0 + 16 * GW * gg + GW * c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            fv v;
+#pragma unroll
+            for (int tw = 0; tw < GW; ++tw) v[tw] = xs[tw][r];
+            fv *dst = (fv *)(vol + (tb + pr[r]) * (size_t)P + qoff);
+            if constexpr (NT) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
+        }
+    };
+    for (int ui = 0; ui < NU; ui += 2) {
+        load_unit(fb, ui + 1);
+        emit(fa, ui);
+        load_unit(fa, ui + 2 < NU ? ui + 2 : 0);
+        emit(fb, ui + 1);
+    }
+}
+
 static bool mf16_eligible(const dm_tiles *b)
 {
     // w0 in {32, 64, 128, 256}: the instantiated column-group counts G = w0/16 = 2, 4, 8, 16

@@ -261,6 +261,32 @@ def test_fused_level2_unsupported_shapes():
     _same(pyr.levels[2][0].cpu().numpy(), lv[2].reshape(pyr.levels[2][0].shape))
 
 
+@pytest.mark.parametrize('h0,w0,ws', [(32, 32, 5), (64, 64, 5), (16, 64, 3), (32, 128, 7),
+                                      (64, 64, 15), (64, 256, 5), (64, 128, 11)])
+@pytest.mark.parametrize('method', [5, 4])
+def test_volume_mfma_equals_generic(h0, w0, ws, method, monkeypatch):
+    """The MFMA level-0 volume kernel (co_map) and per-patch min/max equal the generic
+    kernel's bit for bit, NORMED and CCOEFF; both also against the oracle for one tile."""
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=3 * h0 + w0 + ws, dx=3)
+    # a constant patch (NaN row of the NORMED volume) in tile 0
+    a[2:2 + ws, 5:5 + ws] = 77
+    org = [(0, 0), (4, 8), (2, 3)]
+    res = {}
+    for mode in ('mfq', 'generic'):
+        monkeypatch.setenv('DM_LEVEL1', mode)
+        pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, method), build=False)
+        v = pyr.volume()
+        st = pyr.stats.view(torch.float32)[4 * 3 * h0 * w0:6 * 3 * h0 * w0].cpu().numpy()
+        res[mode] = (v.cpu().numpy(), st)
+    _same(res['mfq'][0], res['generic'][0])
+    _same(res['mfq'][1], res['generic'][1])
+    feat = 'cv2.TM_CCOEFF_NORMED' if method == 5 else 'cv2.TM_CCOEFF'
+    l0 = O.corr_l0(a[:h0 + ws - 1, :w0 + ws - 1], b[:h0 + ws - 1, :w0 + ws - 1], ws, feat)
+    _same(res['mfq'][0][0], l0.reshape(h0 * w0, h0 * w0))
+
+
 @pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (128, 128, 5), (16, 64, 3), (32, 128, 7),
                                       (64, 64, 15), (128, 256, 5)])
 def test_mfma_kernel_equals_generic(h0, w0, ws, monkeypatch):
