@@ -465,6 +465,67 @@ __global__ void k_aggregate(const double *in, int T, int h, int w, int rectify, 
     }
 }
 
+// Same result as k_aggregate, streaming: one workgroup per (tile, output cell, band of
+// output rows), thread (child, v) owns output column v of one child map and walks the
+// band's input rows once (MaxPool columns 2v-1..2v+1, rows streamed), so every input byte
+// is read once from HBM, coalesced.  Children are summed in ul, ur, ll, lr order through
+// LDS.  W2 = w/2 columns per child, 4*W2 threads, BR output rows per band.
+#define AGG_LDS_DOUBLES 4096
+__global__ __launch_bounds__(256) void k_aggregate_rows(const double *in, int T, int h, int w, int BR, int rectify,
+                                                        double *out)
+{
+    __shared__ double pooled[AGG_LDS_DOUBLES]; // [child][band row][v]
+    const int h2 = h / 2, W2 = w / 2;
+    const size_t P = (size_t)h * w, P2 = (size_t)h2 * W2;
+    const int nb = (h2 + BR - 1) / BR;
+    const int band = blockIdx.x % nb, cell = (int)((blockIdx.x / nb) % P2), t = (int)(blockIdx.x / nb / P2);
+    const int I = cell / W2, J = cell % W2;
+    const int tid = threadIdx.x, ch = tid / W2, v = tid % W2;
+    const int u0 = band * BR, u1 = min(u0 + BR, h2);
+    if (ch < 4) {
+        const int cc = (2 * I + (ch >> 1)) * w + 2 * J + (ch & 1);
+        const double *m = in + ((size_t)t * P + cc) * P;
+        double cprev = -INFINITY, R = -INFINITY;
+        const int a0 = max(2 * u0 - 1, 0), a1 = 2 * u1 - 1;
+        constexpr int CH = 8; // rows per batch of loads in flight
+        for (int ab = a0; ab <= a1; ab += CH) {
+            double cmv[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const int a = min(ab + k, a1);
+                const double *row = m + (size_t)a * w;
+                const double x1 = row[2 * v], x2 = row[2 * v + 1], x0 = v > 0 ? row[2 * v - 1] : -INFINITY;
+                cmv[k] = nanmax(nanmax(x0, x1), x2);
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+            const int a = ab + k;
+            if (a > a1) break;
+            const double cm = cmv[k];
+            if ((a & 1) == 0) {
+                R = a == 0 ? cm : nanmax(cprev, cm);
+            } else {
+                if (a >= 2 * u0) {
+                    R = nanmax(R, cm);
+                    pooled[(ch * BR + (a >> 1) - u0) * W2 + v] = R;
+                }
+                cprev = cm;
+            }
+            }
+        }
+    }
+    __syncthreads();
+    const int nout = (u1 - u0) * W2;
+    for (int i = tid; i < nout; i += blockDim.x) {
+        const int ur = i / W2, vv = i % W2;
+        double acc = pooled[(0 * BR + ur) * W2 + vv];
+        acc = acc + pooled[(1 * BR + ur) * W2 + vv];
+        acc = acc + pooled[(2 * BR + ur) * W2 + vv];
+        acc = acc + pooled[(3 * BR + ur) * W2 + vv];
+        out[((size_t)t * P2 + cell) * P2 + (size_t)(u0 + ur) * W2 + vv] = rectify ? pow14(acc / 4.0) : acc / 4.0;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // matching (Matching.py)
 // ------------------------------------------------------------------------------------
@@ -994,6 +1055,17 @@ int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t re
     if (!d_in || !d_out || T < 1 || h < 1 || w < 1) return fail(DM_ERR_ARG, "bad aggregate arguments");
     if ((h & 1) || (w & 1))
         return fail(DM_ERR_SHAPE, "could not broadcast: map side %d must halve (Correlation_map.py:96-103)", (h & 1) ? h : w);
+    const int W2 = w / 2, h2 = h / 2;
+    const char *ag = getenv("DM_AGGREGATE");
+    if (W2 >= 16 && 4 * W2 <= 256 && !(ag && ag[0] == '0')) { // streaming kernel
+        const int BR = AGG_LDS_DOUBLES / (4 * W2) < h2 ? AGG_LDS_DOUBLES / (4 * W2) : h2;
+        const size_t nwg = (size_t)T * h2 * W2 * ((h2 + BR - 1) / BR);
+        if (nwg <= 0x7fffffff) {
+            k_aggregate_rows<<<(unsigned)nwg, 4 * W2, 0, (hipStream_t)stream>>>(d_in, T, h, w, BR, rectify, d_out);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+    }
     const size_t n = (size_t)T * (h / 2) * (w / 2) * (h / 2) * (w / 2);
     k_aggregate<<<nblk(n, 256) > 65536 ? 65536 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_in, T, h, w, rectify, d_out);
     HIP_TRY(hipGetLastError());

@@ -287,6 +287,28 @@ def test_volume_mfma_equals_generic(h0, w0, ws, method, monkeypatch):
     _same(res['mfq'][0][0], l0.reshape(h0 * w0, h0 * w0))
 
 
+@pytest.mark.parametrize('h,w', [(32, 32), (64, 64), (16, 128), (128, 32), (8, 8), (64, 128)])
+@pytest.mark.parametrize('rectify', [1, 0])
+def test_aggregate_streaming_equals_elementwise(h, w, rectify, monkeypatch):
+    """dm_aggregate's streaming kernel (k_aggregate_rows) equals the per-output kernel bit
+    for bit, NaN maps and NaN entries included."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    rng = np.random.default_rng(h * 1000 + w + rectify)
+    T = 2
+    x = rng.random((T, h * w, h * w))
+    x[0, 5] = np.nan                                  # a NaN child map
+    x[1, rng.integers(0, h * w, 40), rng.integers(0, h * w, 40)] = np.nan
+    x[1, 7] = 0.0
+    d = torch.from_numpy(x).cuda()
+    outs = {}
+    for mode in ('1', '0'):
+        monkeypatch.setenv('DM_AGGREGATE', mode)
+        o = torch.empty((T, (h // 2) * (w // 2), (h // 2) * (w // 2)), dtype=torch.float64, device='cuda')
+        L.check(L.load().dm_aggregate(L.ptr(d), T, h, w, rectify, L.ptr(o), L.stream_handle()))
+        outs[mode] = o.cpu().numpy()
+    _same(outs['1'], outs['0'])
+
+
 @pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (128, 128, 5), (16, 64, 3), (32, 128, 7),
                                       (64, 64, 15), (128, 256, 5)])
 def test_mfma_kernel_equals_generic(h0, w0, ws, monkeypatch):

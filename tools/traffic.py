@@ -1,0 +1,34 @@
+"""Per-launch HBM bytes of the level-1 and volume kernels from tools/profile.sh's PMC
+passes: FETCH_SIZE (KiB, x2: gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md HBM
+section) + WRITE_SIZE (KiB).  Writes <dir>/pmc_level1.json and <dir>/pmc_volume.json."""
+import csv
+import json
+import os
+import sys
+
+KERNELS = {'level1': 'k_level1_mfq', 'volume': 'k_volume_mfq'}
+
+
+def per_launch(path, counter, prefix):
+    vals = [float(r['Counter_Value']) for r in csv.DictReader(open(path))
+            if r['Counter_Name'] == counter and r['Kernel_Name'].split('<')[0].split('(')[0].strip()
+            .split()[-1] == prefix]
+    return sum(vals) / len(vals) if vals else None
+
+
+def main(root, tile):
+    for key, prefix in KERNELS.items():
+        f = per_launch(os.path.join(root, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE', prefix)
+        w = per_launch(os.path.join(root, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE', prefix)
+        if f is None or w is None:
+            continue
+        d = {'kernel': prefix, 'tile': tile, 'fetch_kib': f, 'write_kib': w,
+             'hbm_bytes_per_launch': int(2 * f * 1024 + w * 1024),
+             'note': 'FETCH_SIZE x2 (gfx950) + WRITE_SIZE, mean over the launches of bench.py'}
+        with open(os.path.join(root, 'pmc_%s.json' % key), 'w') as fh:
+            json.dump(d, fh, indent=1)
+        print(json.dumps(d))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], int(sys.argv[2]))
