@@ -14,3 +14,18 @@ def lib():
     """Load the HIP library (raises DmUnavailable if it is not built)."""
     from . import _lib
     return _lib.load()
+
+
+def alias_misc():
+    """Make ``import misc.Correlation_map`` (the reference's import style,
+    deep_dem_mathing.py:11-13) resolve to this package's mirror, so reference-side
+    scripts run unchanged on the MI355X engine."""
+    import importlib
+    import sys
+    pkg = importlib.import_module(__name__ + '.misc')
+    sys.modules.setdefault('misc', pkg)
+    for sub in ('Correlation_map', 'Matching', 'Calc_difference', 'Feature_value', 'image_cut_solver',
+                'loader', 'raw_read', 'sub_pix_cal'):
+        mod = importlib.import_module('%s.misc.%s' % (__name__, sub))
+        sys.modules.setdefault('misc.' + sub, mod)
+    return pkg

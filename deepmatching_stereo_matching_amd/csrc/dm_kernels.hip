@@ -897,7 +897,7 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 
 extern "C" {
 
-int dm_abi_version(void) { return 100; }
+int dm_abi_version(void) { return 101; }
 
 const char *dm_last_error(void) { return g_err; }
 

@@ -9,16 +9,9 @@ Documented deviation: the reference's ``assert type(path) == 'str'`` is always f
 """
 
 import numpy as np
-from PIL import Image
 
-
-def _imread_bgr(path):
-    a = np.asarray(Image.open(path).convert('RGB'))
-    return a[:, :, ::-1]  # -> B, G, R like cv2.imread
-
-
-def _imread_gray(path):
-    return np.asarray(Image.open(path).convert('L'))
+from ..imageio import imread_bgr as _imread_bgr
+from ..imageio import imread_gray as _imread_gray
 
 
 class Loader():

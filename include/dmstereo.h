@@ -150,7 +150,7 @@ int dm_stitch(const double *d_match, int32_t n0, int32_t n1, int32_t h0, int32_t
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor). */
+/* ABI version (major * 100 + minor): 101 (1.1 adds dm_corr_level12). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus
