@@ -68,8 +68,10 @@ typedef struct dm_tiles {
     int32_t method;           /* dm_method                                             */
 } dm_tiles;
 
-/* Size in bytes of the per-batch statistics workspace (per-patch / per-window moments,
- * per-patch min/max of the level-0 map): 6 * 4 * T * P. */
+/* Size in bytes of the per-batch statistics workspace: per-patch / per-window moments and
+ * the per-patch min/max of the level-0 map (6 * 4 * T * P), plus, for shapes the MFMA
+ * kernels take, the window operands in MFMA fragment order (T * h0 * (w0/16) * (KS*1024
+ * + 128), KS = ceil(ws^2 / 64)). */
 size_t dm_stats_bytes(const dm_tiles *b);
 
 /* Per-patch and per-window moments.
