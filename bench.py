@@ -47,7 +47,7 @@ def parse():
     ap.add_argument('--tile', type=int, default=S)
     ap.add_argument('--grid', type=int, default=GRID)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-sample-tiles', type=int, default=2)
+    ap.add_argument('--cpu-sample-tiles', type=int, default=16)
     ap.add_argument('--no-volume', action='store_true')
     return ap.parse_args()
 
