@@ -14,6 +14,7 @@
 #pragma once
 
 typedef int dm_v4i __attribute__((ext_vector_type(4)));
+typedef int dm_v2i __attribute__((ext_vector_type(2)));
 
 #define MF_WAVES 4
 
@@ -74,8 +75,10 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
 template <int KS>
 __device__ __forceinline__ void load_frag(dm_v4i *f, const dm_v4i *__restrict__ Bt, int lane)
 {
+    // unsigned lane offset: uniform base + zero-extended 32-bit offset -> saddr loads, no
+    // per-load 64-bit VALU address add
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) f[ks] = Bt[ks * 64 + lane];
+    for (int ks = 0; ks < KS; ++ks) f[ks] = Bt[(unsigned)(ks * 64) + (unsigned)lane];
 }
 
 template <int KS>
@@ -133,6 +136,18 @@ __device__ __forceinline__ dm_v4i mfma16_frag_c(const dm_v4i *A, const dm_v4i *B
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[ks], Bf[ks], acc, 0, 0, 0);
     return acc;
+}
+
+// lane c-1 of the same 16-lane row (DPP row_shr:1, a VALU op; lane c == 0 gets 0)
+__device__ __forceinline__ float dpp_prev16(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+
+// same, lane c == 0 gets `old`
+__device__ __forceinline__ float dpp_prev16_or(float v, float old)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x111, 0xf, 0xf, false));
 }
 
 __device__ __forceinline__ float shfl_prev16(float v, int lane)
@@ -329,7 +344,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
     __shared__ PowLds plds;
-    __shared__ float xch[2][2][NW][4][4]; // [pair parity][row][wave][cell group][child]: y at q1 = 16*GW*(w+1)-1
+    // [pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at q1 = 16*GW*(w+1)-1,
+    // slot 0 = -inf (no window left of column 0)
+    __shared__ __attribute__((aligned(16))) float xch[2][2][NW + 1][4][4];
     __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
     __shared__ double xch2[2][NW][4];  // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
     __shared__ float4 cst[4][6];       // [cell][field][child]: a_p, lo, hi, rmin, den, rinv
@@ -341,10 +358,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     __shared__ double cnan[4];         // [cell]: NaN if a child's map is constant (den == 0), else 0
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
+    if (tid < 64) (&xch[0][0][0][0][0])[(tid >> 4) * (NW + 1) * 16 + (tid & 15)] = -INFINITY;
     __syncthreads();
 
     constexpr int G = GW * NW;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, grp = lane >> 4;
     const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
     const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
@@ -392,12 +410,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         dm_v4i b[GW][KS];
         int2 q[GW];
     };
+    // buffer loads: wave-uniform resource + row offset in SGPRs, lane offset a constant
+    // VGPR -- no per-load VALU address arithmetic
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void *)Bt, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc((void *)Qt, 0, 0x7fffffff, 0x00020000);
+    const unsigned voB = (unsigned)lane * 16u, voQ = (unsigned)c * 8u;
     auto load_row = [&](RowFrag &f, int q0) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const size_t ti = (size_t)q0 * G + tw;
-            load_frag<KS>(f.b[tw], Bt + ti * KS * 64, lane);
-            f.q[tw] = Qt[ti * 16 + c];
+            const unsigned ti = (unsigned)q0 * G + tw;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                f.b[tw][ks] = __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (ti * KS + ks) * 1024u, 0);
+            const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
+            f.q[tw] = make_int2(qv.x, qv.y);
         }
     };
 
@@ -475,9 +501,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     double *L2row = L2F ? L2 + ((size_t)t * P2 + (size_t)(I0 / 2) * w2 + J0 / 2) * P2 : nullptr;
 
     // column MaxPool(3,2,1) of one row on y: Cm[m] over q1 = 2v, 2v+1 and (m >= 1) 2v-1;
-    // the left neighbour of m = 0 (lane c-1's last tile) comes back in prev (lane c == 0:
-    // from wave w-1 through LDS after the barrier), the row's last tile in last.
-    auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&prev)[4], float (&last)[4]) {
+    // the row's last tile comes back in last; the left neighbour of m = 0 (lane c-1's last
+    // tile, or wave w-1's through LDS) is merged after the barrier.
+    auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&last)[4]) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             const dm_v4i acc = mfma16_frag_c<KS>(A, f.b[tw], acc0);
@@ -490,8 +516,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 last[r] = y[r];
             }
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) prev[r] = __shfl(last[r], lane - 1);
     };
 
     // level 2 of this workgroup's cell from level-1 row u (values l1p, lane c == 15's value
@@ -545,24 +569,27 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     for (int q0 = 0; q0 < h0; q0 += 2) {
         const int u = q0 >> 1, k = u & 1;
         load_row(fb, q0 + 1);
-        float Ca[M][4], Cb[M][4], pa[4], pb[4], la[4], lb[4];
-        pool_cols(fa, Ca, pa, la);
+        float Ca[M][4], Cb[M][4], la[4], lb[4];
+        pool_cols(fa, Ca, la);
         if constexpr (!LATE) load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
-        pool_cols(fb, Cb, pb, lb);
+        pool_cols(fb, Cb, lb);
         if (c == 15) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { xch[k][0][wave][grp][r] = la[r]; xch[k][1][wave][grp][r] = lb[r]; }
+            for (int r = 0; r < 4; ++r) { xch[k][0][wave + 1][grp][r] = la[r]; xch[k][1][wave + 1][grp][r] = lb[r]; }
             if (L2F && u > 0) xch2[k ^ 1][wave][grp] = l1p[M - 1];
         }
         __syncthreads();
+        {
+            // left neighbour of pooled column 0: lane c-1's last tile (DPP row_shr:1); lane
+            // c == 0 keeps the DPP "old" operand = wave w-1's edge value (slot w; -inf for w = 0)
+            const float4 xa = *(const float4 *)&xch[k][0][wave][grp][0];
+            const float4 xb = *(const float4 *)&xch[k][1][wave][grp][0];
+            const float oa[4] = {xa.x, xa.y, xa.z, xa.w}, ob[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (c == 0) {
-                pa[r] = wave == 0 ? -INFINITY : xch[k][0][wave - 1][grp][r];
-                pb[r] = wave == 0 ? -INFINITY : xch[k][1][wave - 1][grp][r];
+            for (int r = 0; r < 4; ++r) {
+                Ca[0][r] = fmaxf(Ca[0][r], dpp_prev16_or(la[r], oa[r]));
+                Cb[0][r] = fmaxf(Cb[0][r], dpp_prev16_or(lb[r], ob[r]));
             }
-            Ca[0][r] = fmaxf(Ca[0][r], pa[r]);
-            Cb[0][r] = fmaxf(Cb[0][r], pb[r]);
         }
         double l1q[M]; // level-1 row u - 1, consumed by level2_row below
 #pragma unroll
@@ -685,7 +712,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
         for (int tw = 0; tw < GW; ++tw) {
             const size_t ti = (size_t)q0 * G + gg * GW + tw;
             load_frag<KS>(f.b[tw], Bt + ti * KS * 64, lane);
-            f.q[tw] = Qt[ti * 16 + c];
+            f.q[tw] = (Qt + ti * 16)[(unsigned)c];
         }
     };
 
