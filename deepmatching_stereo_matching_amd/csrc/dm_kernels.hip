@@ -1014,15 +1014,17 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         const int KS = (b->ws * b->ws + 63) / 64, GW = b->w0 / 16 / mfq_nw(b);
         const size_t waves = (size_t)b->T * (b->h0 / 4) * (b->w0 / 4);
         const unsigned vgrid = (unsigned)((waves + 3) / 4);
-        const char *nt = getenv("DM_VOLUME_NT");
+        const char *nt = getenv("DM_VOLUME_NT"), *ls = getenv("DM_VOLUME_LS");
         const bool ntst = !(nt && nt[0] == '0');
+        const bool lds = !(ls && ls[0] == '0') && b->w0 <= 128; // stage: 16 x w0 floats per wave
         const bool yf = b->ws <= 5;
         const Geo gg = make_geo(b);
         hipStream_t st = (hipStream_t)stream;
-#define DM_VQ(KS_, GW_, YF_, NT_) if (KS == KS_ && GW == GW_ && yf == YF_ && ntst == NT_) { k_volume_mfq<KS_, GW_, YF_, NT_><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0); HIP_TRY(hipGetLastError()); return DM_OK; }
-        DM_VQ(1, 2, true, true) DM_VQ(1, 4, true, true) DM_VQ(1, 2, true, false) DM_VQ(1, 4, true, false)
-        DM_VQ(1, 2, false, true) DM_VQ(1, 4, false, true) DM_VQ(2, 2, false, true) DM_VQ(2, 4, false, true)
-        DM_VQ(3, 2, false, true) DM_VQ(3, 4, false, true) DM_VQ(4, 2, false, true) DM_VQ(4, 4, false, true)
+#define DM_VQ(KS_, GW_, YF_, NT_, LS_) if (KS == KS_ && GW == GW_ && yf == YF_ && ntst == NT_ && lds == LS_) { k_volume_mfq<KS_, GW_, YF_, NT_, LS_><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0); HIP_TRY(hipGetLastError()); return DM_OK; }
+        DM_VQ(1, 2, true, true, true) DM_VQ(1, 2, true, true, false) DM_VQ(1, 2, true, false, true) DM_VQ(1, 2, true, false, false)
+        DM_VQ(1, 4, true, true, false) DM_VQ(1, 4, true, false, false)
+        DM_VQ(1, 2, false, true, true) DM_VQ(1, 4, false, true, false) DM_VQ(2, 2, false, true, true) DM_VQ(2, 4, false, true, false)
+        DM_VQ(3, 2, false, true, true) DM_VQ(3, 4, false, true, false) DM_VQ(4, 2, false, true, true) DM_VQ(4, 4, false, true, false)
 #undef DM_VQ
     }
     k_minmax<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s);

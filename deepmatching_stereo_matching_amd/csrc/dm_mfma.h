@@ -652,17 +652,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 // lane c's GW tiles of group g are GW consecutive floats: one GW-float vector store per
 // patch, a 16-lane group writing 64*GW/... = 16*GW*4 contiguous bytes of the patch's row.
 // ===================================================================================
-template <int KS, int GW, bool YF, bool NT>
+template <int KS, int GW, bool YF, bool NT, bool LS>
 __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                     const int2 *__restrict__ QS, float *vol)
 {
-    const int lane = threadIdx.x & 63;
+    // LS: a row's 16 x w0 results are staged in LDS and stored as whole patch rows
+    // (w0 * 4 contiguous bytes per patch, 16-B lanes) instead of GW-float pieces
+    __shared__ __attribute__((aligned(16))) float stage[LS ? 4 : 1][LS ? 16 * 128 : 1];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int c = lane & 15, grp = lane >> 4;
     const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
     const int G = w0 / 16, NG = G / GW; // tiles per row, column groups per row
     const int nbj = w0 / 4, bpt = (h0 / 4) * nbj;
-    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wid >= g.T * bpt) return; // whole wave
+    const int wid = blockIdx.x * 4 + wv;
+    if (wid >= g.T * bpt) return; // whole wave (no barrier in this kernel)
     const int t = wid / bpt;
     const int I0 = 2 * ((wid % bpt) / nbj), J0 = 2 * ((wid % bpt) % nbj);
     const size_t tb = (size_t)t * P;
@@ -697,8 +700,11 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     }
     const int ab = YF ? DM_YBIAS : 0;
     const dm_v4i acc0 = {ab, ab, ab, ab};
-    const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
-    const int2 *Qt = QS + (size_t)t * h0 * G * 16;
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(Bw + (size_t)t * h0 * G * KS * 64), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rQ =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(QS + (size_t)t * h0 * G * 16), 0, 0x7fffffff, 0x00020000);
+    const unsigned voB = (unsigned)lane * 16u, voQ = (unsigned)c * 8u;
 
     // unit = (row q0, column group gg): GW tiles; double-buffered loads
     struct Unit {
@@ -707,12 +713,14 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     };
     const int NU = h0 * NG;
     auto load_unit = [&](Unit &f, int uidx) {
-        const int q0 = uidx / NG, gg = uidx % NG;
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const size_t ti = (size_t)q0 * G + gg * GW + tw;
-            load_frag<KS>(f.b[tw], Bt + ti * KS * 64, lane);
-            f.q[tw] = (Qt + ti * 16)[(unsigned)c];
+            const unsigned ti = (unsigned)uidx * GW + tw; // = q0 * G + gg * GW + tw
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                f.b[tw][ks] = __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (ti * KS + ks) * 1024u, 0);
+            const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
+            f.q[tw] = make_int2(qv.x, qv.y);
         }
     };
 
@@ -760,6 +768,8 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     }
 
     typedef float fv __attribute__((ext_vector_type(GW)));
+    float *stg = &stage[LS ? wv : 0][0];
+    const size_t pbase = tb + (size_t)(2 * I0) * w0 + 2 * J0; // patch (row 2*I0, col 2*J0)
     auto emit = [&](const Unit &f, int uidx) {
         const int q0 = uidx / NG, gg = uidx % NG;
         float xs[GW][4];
@@ -773,15 +783,39 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
                 xs[tw][r] = norm_mk(rr, rmn[r], den[r], rinv[r]);
             }
         }
-        const size_t qoff = (size_t)q0 * w0 + 16 * GW * gg + GW * c;
+        const int col = 16 * GW * gg + GW * c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             fv v;
 #pragma unroll
             for (int tw = 0; tw < GW; ++tw) v[tw] = xs[tw][r];
-            fv *dst = (fv *)(vol + (tb + pr[r]) * (size_t)P + qoff);
-            if constexpr (NT) __builtin_nontemporal_store(v, dst);
-            else *dst = v;
+            if constexpr (LS) {
+                *(fv *)(stg + (4 * grp + r) * w0 + col) = v;
+            } else {
+                fv *dst = (fv *)(vol + (tb + pr[r]) * (size_t)P + (size_t)q0 * w0 + col);
+                if constexpr (NT) __builtin_nontemporal_store(v, dst);
+                else *dst = v;
+            }
+        }
+        if constexpr (LS) {
+            if (gg == NG - 1) { // the row is complete: 16 patch rows of w0 floats
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int per = w0 / 4;            // float4 per patch row
+                const int rows_per = 64 / per;     // patch rows per store instruction
+                for (int j = 0; j < 16; j += rows_per) {
+                    const int pl = j + lane / per, k4 = lane % per; // local patch 4*cell + child
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const f4v v4 = *(const f4v *)(stg + pl * w0 + 4 * k4);
+                    const int pc = pl >> 2, pch = pl & 3;
+                    const size_t prow = pbase + (size_t)(2 * (pc >> 1) + (pch >> 1)) * w0 + 2 * (pc & 1) + (pch & 1);
+                    f4v *dst = (f4v *)(vol + prow * (size_t)P + (size_t)q0 * w0) + k4;
+                    if constexpr (NT) __builtin_nontemporal_store(v4, dst);
+                    else *dst = v4;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
     };
     for (int ui = 0; ui < NU; ui += 2) {
