@@ -17,6 +17,7 @@ import torch
 from . import _lib as L
 
 LAM = 1.4
+FUSE_DEFAULT = 1   # DevicePyramid level-1/level-2 mode (see its docstring); 1 is fastest on C3
 
 
 def default_device():
@@ -85,12 +86,13 @@ class DevicePyramid:
     """co_map_list of a TileBatch, resident on the device.
 
     levels[0] is never stored (the fused kernels do not write level 0; matching evaluates
-    it on demand).  With ``fuse_level2`` (env DM_FUSE_L2=1) and a shape the fused
-    level-1/level-2 kernel supports, level 1 stays on chip as well (levels[1] is None until
-    ``level(1)`` asks for it).  Off by default: on the C3 workload the fused kernel's extra
-    register pressure (4 instead of 5 waves/SIMD) costs more (~1.1 ms/pair) than writing
-    level 1 and pooling it with dm_aggregate (~0.8 ms/pair).  levels[l] for the others are
-    float64 [T][Pl][Pl] tensors."""
+    it on demand).  ``fuse_level2`` (env DM_FUSE_L2) selects how levels 1-2 are built, on
+    shapes the fused level-1/level-2 kernel supports:
+      0  dm_corr_level1 writes level 1, dm_aggregate pools it into level 2;
+      1  dm_corr_level12 writes levels 1 and 2 in one pass (no level-1 re-read);
+      2  dm_corr_level12 writes level 2 only: level 1 stays on chip (levels[1] is None
+         until ``level(1)`` asks for it) and matching evaluates it on demand.
+    levels[l] for the others are float64 [T][Pl][Pl] tensors."""
 
     def __init__(self, batch, stream=None, build=True, fuse_level2=None):
         self.b = batch
@@ -100,8 +102,8 @@ class DevicePyramid:
         self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
                                  device=batch.device)
         if fuse_level2 is None:
-            fuse_level2 = os.environ.get('DM_FUSE_L2', '0') == '1'
-        self.fuse_level2 = bool(fuse_level2)
+            fuse_level2 = int(os.environ.get('DM_FUSE_L2', str(FUSE_DEFAULT)))
+        self.fuse_level2 = int(fuse_level2)
         self.levels = [None]
         self._volume = None
         self._have_minmax = False
@@ -144,9 +146,10 @@ class DevicePyramid:
                 events[0].record(st)
             if self.fuse_level2 and self.nlev >= 3:
                 l2 = self._empty_level(2)
-                rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), None, L.ptr(l2), self._s())
+                l1 = self._empty_level(1) if self.fuse_level2 == 1 else None
+                rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), L.ptr(l1), L.ptr(l2), self._s())
                 if rc == L.DM_OK:
-                    self.levels += [None, l2]
+                    self.levels += [l1, l2]
                     self._have_minmax = True
                     h, w, fused = h // 2, w // 2, True
                 elif rc != L.DM_ERR_UNSUPPORTED:

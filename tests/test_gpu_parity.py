@@ -224,9 +224,12 @@ def test_fused_level2_equals_aggregate(h0, w0, ws):
     from deepmatching_stereo_matching_amd.synthetic import stereo_pair
     a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=7 * h0 + w0 + ws, dx=3)
     org = [(0, 0), (4, 8), (2, 3)]
-    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=False)
-    fused = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=True)
+    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=0)
+    fused = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=2)
+    both = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=1)
     assert fused.levels[1] is None and ref.levels[1] is not None
+    _same(both.levels[1].cpu().numpy(), ref.levels[1].cpu().numpy())
+    _same(both.match().cpu().numpy(), ref.match().cpu().numpy())
     for k in range(2, ref.nlev):
         _same(fused.levels[k].cpu().numpy(), ref.levels[k].cpu().numpy())
     _same(fused.match().cpu().numpy(), ref.match().cpu().numpy())
@@ -251,7 +254,7 @@ def test_fused_level2_unsupported_shapes():
     from deepmatching_stereo_matching_amd.synthetic import stereo_pair
     a, b = stereo_pair(60, 110, seed=3, dx=2)
     batch = engine.TileBatch(a, b, [(0, 0)], 32, 96, 5, 5)   # w0 = 96: not a power of two
-    pyr = engine.DevicePyramid(batch, fuse_level2=True)
+    pyr = engine.DevicePyramid(batch, fuse_level2=2)
     assert pyr.levels[1] is not None
     l2 = torch.empty((1, 8 * 24, 8 * 24), dtype=torch.float64, device='cuda')
     rc = L.load().dm_corr_level12(batch.ref(), L.ptr(pyr.stats), None, L.ptr(l2), L.stream_handle())
