@@ -615,6 +615,86 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, in
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
 }
 
+// The _B step onto level 1 when level 1 was never stored (dm_corr_level12 without level 1):
+// four lanes per entry, one per child patch of the level-1 cell.  A lane computes y on the
+// 7x7 level-0 neighbourhood its entry's 3x3 level-1 window pools from, takes the MaxPool on
+// y (monotone: same as pooling the rectified values), normalises and rectifies the 9 pooled
+// values; the 4 lanes sum them in ul, ur, ll, lr order, /4, rectify -- the arithmetic of
+// k_level1_mfq / k_aggregate, so the window equals the stored level 1 bit for bit.
+template <int WS>
+__global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
+{
+    constexpr int ws = WS, n = WS * WS;
+    const int h0 = g.h0, w0 = g.w0;
+    const int h1 = h0 / 2, w1 = w0 / 2, h = h1 / 2, w = w1 / 2;
+    const size_t P = (size_t)h0 * w0, P1 = (size_t)h1 * w1, Pp = (size_t)h * w;
+    const size_t gid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t e = gid >> 2;
+    const int ch = (int)(gid & 3);
+    const bool live = e < (size_t)T * P1;
+    const size_t ee = live ? e : 0;
+    const int t = (int)(ee / P1), pc = (int)(ee % P1);
+    const int p0 = pc / w1, p1 = pc % w1;
+    const double *pm = pmap + (size_t)t * 3 * Pp;
+    const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
+    const int pd0 = (int)(long long)(pm[par] * 2) + (p0 & 1);
+    const int pd1 = (int)(long long)(pm[Pp + par] * 2) + (p1 & 1);
+    // child patch (level-0 patch coordinates) and its statistics
+    const int pp0 = 2 * p0 + (ch >> 1), pp1 = 2 * p1 + (ch & 1);
+    const size_t op = (size_t)t * P + (size_t)pp0 * w0 + pp1;
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+    int T8[n];
+    {
+        const uint8_t *a = g.img1 + (size_t)(ro + pp0) * g.pitch1 + co + pp1;
+#pragma unroll
+        for (int k = 0; k < n; ++k) T8[k] = (int)a[(size_t)(k / ws) * g.pitch1 + (k % ws)] - 128;
+    }
+    const int sT = s.sT[op];
+    const float ap = s.aP[op], rmn = s.rmn[op], rmx = s.rmx[op];
+    // y on level-0 rows/cols 2*pd - 3 .. 2*pd + 3 (-inf outside the map)
+    float y[7][7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const int qa = 2 * pd0 - 3 + i, qb = 2 * pd1 - 3 + j;
+            if (qa < 0 || qa >= h0 || qb < 0 || qb >= w0) { y[i][j] = -INFINITY; continue; }
+            const uint8_t *b = g.img2 + (size_t)(ro + qa) * g.pitch2 + co + qb;
+            int acc = 0;
+#pragma unroll
+            for (int k = 0; k < n; ++k) acc += T8[k] * ((int)b[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128);
+            const size_t oq = (size_t)t * P + (size_t)qa * w0 + qb;
+            y[i][j] = y_of_num(n * acc - sT * s.sI[oq], s.bQ[oq]);
+        }
+    double win[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const int u = pd0 - 1 + a, v = pd1 - 1 + b;
+            double pv = 0.0;
+            const bool in = u >= 0 && u < h1 && v >= 0 && v < w1;
+            if (in) {
+                float R = -INFINITY;
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) R = fmaxf(R, y[2 * a + i][2 * b + j]);
+                pv = pow14((double)norm_x(r_of_y(R, ap, g.method), rmn, rmx));
+            }
+            // children sum in ul, ur, ll, lr order (lanes 4e + 0..3)
+            const int base = (threadIdx.x & 63) & ~3;
+            const double v0 = __shfl(pv, base), v1 = __shfl(pv, base + 1), v2 = __shfl(pv, base + 2),
+                         v3 = __shfl(pv, base + 3);
+            win[a * 3 + b] = in ? pow14((((v0 + v1) + v2) + v3) / 4.0) : 0.0;
+        }
+    if (!live || ch != 0) return;
+    double o[3];
+    near_pick(win, pd0, pd1, o);
+    double *cm_ = cmap + (size_t)t * 3 * P1;
+    cm_[pc] = o[0]; cm_[P1 + pc] = o[1]; cm_[2 * P1 + pc] = o[2];
+}
+
 // Matching._sub_pix_cal (:177-209) on the final level-0 map, in place.  L0: materialised
 // rectified level 0 ([T][P][P]) or nullptr (on demand from images + stats).
 __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, double *map)
@@ -871,8 +951,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
-    // register budget: 5 waves/SIMD without the level-2 tail, 4 with it (5 spills there)
-#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, L2F ? 4 : 5, L2F, YF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    // register budget: 5 waves/SIMD (measured best for both variants on C3)
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4)
     if constexpr (!YF) {
         DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4)
@@ -1125,7 +1205,23 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
     if (rc) return rc;
     for (int l = K - 1; l >= 0; --l) {
         const size_t n = (size_t)T * (2 * h) * (2 * w);
-        k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
+        if (l == 1 && !d_levels[1]) { // level 1 on demand: dedicated 4-lanes-per-entry kernel
+            const unsigned nb = nblk(4 * n, 256);
+            switch (g.ws) {
+            case 1: k_match_step_l1<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 3: k_match_step_l1<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 5: k_match_step_l1<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 7: k_match_step_l1<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 9: k_match_step_l1<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 11: k_match_step_l1<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 13: k_match_step_l1<13><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 15: k_match_step_l1<15><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            default:
+                k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
+            }
+        } else {
+            k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
+        }
         HIP_TRY(hipGetLastError());
         cur ^= 1;
         h *= 2; w *= 2;

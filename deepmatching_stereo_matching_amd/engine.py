@@ -17,7 +17,7 @@ import torch
 from . import _lib as L
 
 LAM = 1.4
-FUSE_DEFAULT = 1   # DevicePyramid level-1/level-2 mode (see its docstring); 1 is fastest on C3
+FUSE_DEFAULT = 2   # DevicePyramid level-1/level-2 mode (see its docstring); 2 is fastest on C3
 
 
 def default_device():
