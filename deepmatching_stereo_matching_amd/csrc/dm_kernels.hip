@@ -70,8 +70,7 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
 __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
 {
     const double r = fma(M, t.fc[i], -1.0);
-    double q = DM_POWF_B6;
-    q = fma(q, r, DM_POWF_B5);
+    double q = DM_POWF_B5;
     q = fma(q, r, DM_POWF_B4);
     q = fma(q, r, DM_POWF_B3);
     q = fma(q, r, DM_POWF_B2);

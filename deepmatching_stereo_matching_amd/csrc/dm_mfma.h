@@ -29,7 +29,7 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 // ===================================================================================
 
 // Bw16[t][q0][tau][ks][lane] (16 B): lane L = c + 16 hq holds taps k = 64 ks + 16 hq + j of
-// window (q0, G*c + tau);  QS16[t][q0][tau][c] = { -sum(I'), bits(b_q) }.
+// window (q0, G*c + tau);  QS16[t][q0][tau][c] = { bits(f32(-sum(I'))), bits(b_q) }.
 // Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
 // lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
 // GW = G/NW: one group per wave of k_level1_mfq.
@@ -55,7 +55,7 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
     float bq;
     if (g.method == DM_TM_CCOEFF) bq = 1.0f;
     else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
-    QS[idx] = make_int2(-s, __float_as_int(bq));
+    QS[idx] = make_int2(__float_as_int((float)-s), __float_as_int(bq)); // exact: |s| <= 225*128
     const size_t tile = idx / 16; // (t, q0, tau)
     for (int ks = 0; ks < KS; ++ks)
         for (int hq = 0; hq < 4; ++hq) {
@@ -102,7 +102,7 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
 // y = f32(num) * b_q for the 4 patches (acc[r]) of one lane against its window (qs).
 // YF (n <= 25): acc was accumulated onto DM_YBIAS, so its bits read as the float
 // 1.5*2^23 + acc (exact for |acc| <= 128^2 n < 2^22); with sTf = f32(sum T') and
-// -sum(I') = qs.x, sT*sI is exact in f32 (|.| <= (128 n)^2 < 2^24) and
+// -sum(I') = f32 bits in qs.x, sT*sI is exact in f32 (|.| <= (128 n)^2 < 2^24) and
 // fma(acc, n, -sT sI) rounds the exact integer num once -- the same f32(num) as the
 // integer path, in packed-f32 instructions (2 voxels each).
 #define DM_YBIAS 0x4B400000
@@ -114,7 +114,7 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
 {
     const float b = __int_as_float(qs.y);
     if constexpr (YF) {
-        const float nf = (float)n, sI = (float)qs.x;
+        const float nf = (float)n, sI = __int_as_float(qs.x);
         const dm_f2 bias = {12582912.0f, 12582912.0f};
         const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])} - bias;
         const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])} - bias;
@@ -126,7 +126,8 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
         y[0] = y01.x; y[1] = y01.y; y[2] = y23.x; y[3] = y23.y;
     } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+        for (int r = 0; r < 4; ++r)
+            y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
     }
 }
 
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
         const float b = __int_as_float(qs.y);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+            const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
             mn[r] = fminf(mn[r], y);
             mx[r] = fmaxf(mx[r], y);
         }
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
             const float b = __int_as_float(qs.y);
             float y[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], qs.x)), b);
+            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
             if (it == 0) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { xlast[r] = y[r]; prev[r] = shfl_prev16(y[r], lane); }

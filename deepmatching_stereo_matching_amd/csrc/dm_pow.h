@@ -49,7 +49,7 @@ DM_HD static inline double dm_f64_bits(uint64_t b)
     return x;
 }
 
-/* fast path, x in [2^DM_POWF_EMIN, 1]: one table row, degree-6 series, one 2^(yE) row */
+/* fast path, x in [2^DM_POWF_EMIN, 1]: one table row, degree-5 series, one 2^(yE) row */
 DM_HD static inline double dm_pow14_fast(double x, const double *fc, const double *fp, const double *fg)
 {
     const uint64_t b = dm_bits_f64(x);
@@ -57,8 +57,7 @@ DM_HD static inline double dm_pow14_fast(double x, const double *fc, const doubl
     const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
     const int i = (int)((b >> 43) & (DM_POWF_NT - 1));
     const double r = fma(M, fc[i], -1.0);                  /* |r| <= 2^-10 */
-    double q = DM_POWF_B6;
-    q = fma(q, r, DM_POWF_B5);
+    double q = DM_POWF_B5;
     q = fma(q, r, DM_POWF_B4);
     q = fma(q, r, DM_POWF_B3);
     q = fma(q, r, DM_POWF_B2);
