@@ -188,12 +188,14 @@ def main():
     value = world * args.steps * voxels / elapsed / 1e9
     l1_ms = solver.level1_ms()
     if rank == 0:
-        # dominant kernel: the fused level-0 -> level-1 kernel.  Algorithmic bytes per
+        # dominant kernel: the fused level-0 -> level-1 (-> level-2) kernel.  Algorithmic bytes per
         # 4 B per level-0 voxel (the volume a materialising L0 kernel
         # writes); this kernel keeps level 0 on chip, so "achieved" is the HBM-equivalent
         # rate and "traffic" (PMC) the bytes it really moves.
         gbs = 4.0 * voxels / (l1_ms * 1e-3) / 1e9
-        roof = {'kernel': 'dm_corr_level1 (k_level1_mfq)', 'bound': 'hbm', 'ms': round(l1_ms, 3),
+        mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
+        kname = 'dm_corr_level1 (k_level1_mfq)' if mode == 0 else 'dm_corr_level12 (k_level1_mfq, level 2 fused)'
+        roof = {'kernel': kname, 'bound': 'hbm', 'ms': round(l1_ms, 3),
                 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(tile),
                 'algorithmic': '4 B/voxel x %d voxels per launch (level 0 never leaves the chip)'
