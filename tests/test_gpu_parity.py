@@ -290,6 +290,27 @@ def test_volume_mfma_equals_generic(h0, w0, ws, method, monkeypatch):
     _same(res['mfq'][0][0], l0.reshape(h0 * w0, h0 * w0))
 
 
+def test_s256_tile_paths_agree(monkeypatch):
+    """C5-sized tile (S = 256, GW = 4 instances): the column-split kernel, the independent
+    one-wave-per-4-cells kernel (mf16) and the fused level-2 path agree bit for bit."""
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    S, ws = 256, 5
+    a, b = stereo_pair(S + ws - 1, S + ws - 1, seed=256, dx=3, sinusoidal=True)
+    res = {}
+    for var in ('mfq', 'mf16'):
+        monkeypatch.setenv('DM_LEVEL1', var)
+        pyr = engine.DevicePyramid(engine.TileBatch(a, b, [(0, 0)], S, S, ws, 5), fuse_level2=0)
+        res[var] = (pyr.levels[1][0, ::97].cpu().numpy(), pyr.levels[2].cpu().numpy(), pyr.match().cpu().numpy())
+        del pyr
+    for x, y in zip(res['mfq'], res['mf16']):
+        _same(x, y)
+    monkeypatch.setenv('DM_LEVEL1', 'mfq')
+    fused = engine.DevicePyramid(engine.TileBatch(a, b, [(0, 0)], S, S, ws, 5), fuse_level2=2)
+    _same(fused.levels[2].cpu().numpy(), res['mfq'][1])
+    _same(fused.match().cpu().numpy(), res['mfq'][2])
+
+
 @pytest.mark.parametrize('h,w', [(32, 32), (64, 64), (16, 128), (128, 32), (8, 8), (64, 128)])
 @pytest.mark.parametrize('rectify', [1, 0])
 def test_aggregate_streaming_equals_elementwise(h, w, rectify, monkeypatch):
