@@ -919,6 +919,99 @@ static inline unsigned nblk(size_t n, unsigned bs)
     return (unsigned)(b > 0x7fffffff ? 0x7fffffff : b);
 }
 
+// Level-0 values of one patch on demand with its taps in registers (WS known at compile
+// time): the same expression as l0_value.
+template <int WS>
+struct PatchL0 {
+    int T8[WS * WS];
+    int sT;
+    float ap, rmn, rmx;
+    __device__ void load(const Geo &g, const Stats &s, int t, int p0, int p1)
+    {
+        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+        const uint8_t *a = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+#pragma unroll
+        for (int k = 0; k < WS * WS; ++k) T8[k] = (int)a[(size_t)(k / WS) * g.pitch1 + (k % WS)] - 128;
+        const size_t op = (size_t)t * g.h0 * g.w0 + (size_t)p0 * g.w0 + p1;
+        sT = s.sT[op]; ap = s.aP[op]; rmn = s.rmn[op]; rmx = s.rmx[op];
+    }
+    __device__ double value(const Geo &g, const Stats &s, int t, int q0, int q1) const
+    {
+        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+        const uint8_t *b = g.img2 + (size_t)(ro + q0) * g.pitch2 + co + q1;
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < WS * WS; ++k) acc += T8[k] * ((int)b[(size_t)(k / WS) * g.pitch2 + (k % WS)] - 128);
+        const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
+        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
+        return pow14((double)norm_x(r, rmn, rmx));
+    }
+};
+
+// the last _B step (onto level 0) with level 0 on demand, patch taps in registers
+template <int WS>
+__global__ __launch_bounds__(256) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
+{
+    const int hn = g.h0, wn = g.w0, h = hn / 2, w = wn / 2;
+    const size_t Pp = (size_t)h * w, Pn = (size_t)hn * wn;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * Pn) return;
+    const int t = (int)(idx / Pn), pc = (int)(idx % Pn);
+    const int p0 = pc / wn, p1 = pc % wn;
+    const double *pm = pmap + (size_t)t * 3 * Pp;
+    const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
+    const int pd0 = (int)(long long)(pm[par] * 2) + (p0 & 1);
+    const int pd1 = (int)(long long)(pm[Pp + par] * 2) + (p1 & 1);
+    PatchL0<WS> pt;
+    pt.load(g, s, t, p0, p1);
+    double win[9], o[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const int r = pd0 - 1 + a, c = pd1 - 1 + b;
+            win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0 : pt.value(g, s, t, r, c);
+        }
+    near_pick(win, pd0, pd1, o);
+    double *cm_ = cmap + (size_t)t * 3 * Pn;
+    cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
+}
+
+// _sub_pix_cal with level 0 on demand, patch taps in registers (see k_subpix)
+template <int WS>
+__global__ __launch_bounds__(256) void k_subpix_t(Geo g, Stats s, int T, double *map)
+{
+    const int h0 = g.h0, w0 = g.w0;
+    const size_t P = (size_t)h0 * w0;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    const int t = (int)(idx / P), pc = (int)(idx % P);
+    const int p0 = pc / w0, p1 = pc % w0;
+    double *mt = map + (size_t)t * 3 * P;
+    PatchL0<WS> pt;
+    pt.load(g, s, t, p0, p1);
+    const double row = mt[pc], col = mt[P + pc];
+    const int c0 = (int)row, c1 = (int)col;
+    const double r0 = pt.value(g, s, t, c0, c1);
+    const double dx = (double)p0 - row;
+    double nrow, ncol;
+    if (c0 + 1 >= h0) {
+        nrow = (double)p0 - dx;
+    } else {
+        const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1;
+        nrow = ((double)p0 - dx) + sub_pix_compute(r0, pt.value(g, s, t, c0 + 1, c1), pt.value(g, s, t, cm, c1));
+    }
+    const double dy = (double)p1 - col;
+    if (c1 + 1 >= w0) {
+        ncol = (double)p1 - dy;
+    } else {
+        const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
+        ncol = ((double)p1 - dy) + sub_pix_compute(r0, pt.value(g, s, t, c0, c1 + 1), pt.value(g, s, t, c0, cm));
+    }
+    mt[pc] = nrow;
+    mt[P + pc] = ncol;
+}
+
 template <int WS>
 static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 {
@@ -1218,6 +1311,18 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             default:
                 k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
             }
+        } else if (l == 0 && !d_levels[0] && g.ws <= 15) { // level 0 on demand, taps in registers
+            const unsigned nb = nblk(n, 256);
+            switch (g.ws) {
+            case 1: k_match_step_l0<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 3: k_match_step_l0<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 5: k_match_step_l0<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 7: k_match_step_l0<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 9: k_match_step_l0<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 11: k_match_step_l0<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 13: k_match_step_l0<13><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            default: k_match_step_l0<15><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            }
         } else {
             k_match_step<<<nblk(n, 64), 64, 0, st>>>(g, s, d_levels[l], l, T, h, w, buf[cur], buf[cur ^ 1]);
         }
@@ -1228,7 +1333,21 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
         if (rc) return rc;
     }
     if (sub_pix) {
-        k_subpix<<<nblk((size_t)T * h0 * w0, 64), 64, 0, st>>>(g, s, d_levels[0], T, h0, w0, buf[cur]);
+        const unsigned nb = nblk((size_t)T * h0 * w0, 256);
+        if (!d_levels[0]) {
+            switch (g.ws) {
+            case 1: k_subpix_t<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 3: k_subpix_t<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 5: k_subpix_t<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 7: k_subpix_t<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 9: k_subpix_t<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 11: k_subpix_t<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 13: k_subpix_t<13><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            default: k_subpix_t<15><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            }
+        } else {
+            k_subpix<<<nblk((size_t)T * h0 * w0, 64), 64, 0, st>>>(g, s, d_levels[0], T, h0, w0, buf[cur]);
+        }
         HIP_TRY(hipGetLastError());
     }
     if (buf[cur] != d_out)
