@@ -37,6 +37,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 WS = 5
 S = 128
 GRID = 8
+CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
+VOLUME_BUDGET = 64e9           # bytes of level-0 volume materialised for its roofline
 
 
 def parse():
@@ -44,8 +46,11 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--tile', type=int, default=S)
-    ap.add_argument('--grid', type=int, default=GRID)
+    ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
+                    help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
+                         'c5 (4096^2, S=256)')
+    ap.add_argument('--tile', type=int, default=None)
+    ap.add_argument('--grid', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample-tiles', type=int, default=16)
     ap.add_argument('--no-volume', action='store_true')
@@ -84,7 +89,10 @@ class PairSolver:
 def volume_roofline(solver, reps=3):
     """HBM roofline of the level-0 volume kernel (dm_corr_volume: co_map, float32, written in
     full) on the same C3 batch: 4 B per voxel written."""
-    batch = solver.batch
+    full = solver.batch
+    nt = max(1, min(full.T, int(VOLUME_BUDGET // (4.0 * full.P * full.P))))
+    batch = engine.TileBatch(full.img1, full.img2, full.origins_host[:nt], full.h0, full.w0, full.ws,
+                             full.method, full.device)
     pyr = engine.DevicePyramid(batch, build=False)
     pyr.compute_stats()
     vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=batch.device)
@@ -156,7 +164,8 @@ def main():
     dev = torch.device('cuda', local if dist else 0)
     torch.cuda.set_device(dev)
 
-    tile, grid = args.tile, args.grid
+    tile, grid = CONFIGS[args.config]
+    tile, grid = args.tile or tile, args.grid or grid
     # ImageCutSolver's floor rule (image_cut_solver.py:62): floor((side - (tile+ws-1)) / tile)
     # tiles per axis, so a grid x grid cut needs side = (grid+1)*tile + ws-1 (1156 for C3)
     side = (grid + 1) * tile + WS - 1
@@ -205,15 +214,15 @@ def main():
                'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
                'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
                'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
-               'config': {'workload': 'C3: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
+               'config': {'workload': '%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
                                       '+ sub-pixel + cal_map + stitch'
-                                      % (grid * tile, grid * tile, grid, grid, tile, WS),
+                                      % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS),
                           'tile': tile, 'tiles_per_pair': grid * grid, 'window_size': WS,
                           'pairs_per_gpu_per_step': 1, 'parallelism': 'pairs sharded %d-way' % world},
                'roofline': roof}
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and tile <= 128:   # S=256: 17 GB level 0 per tile on the host
             rec['cpu_baseline'] = cpu_baseline(args.cpu_sample_tiles, tile)
         print(json.dumps(rec))
     if dist:
