@@ -1188,6 +1188,27 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
+        const char *cs = getenv("DM_VOLUME_CS");
+        const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
+        if (!(cs && cs[0] == '0') && b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
+            // column-split workgroups with a shared LDS stage (RB rows per store burst)
+            const unsigned cgrid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
+            const Geo gc = make_geo(b);
+            hipStream_t sc = (hipStream_t)stream;
+            const char *rbe = getenv("DM_VOLUME_RB"); // A/B knob: rows per store burst (C3 shape)
+            const int rb = rbe ? atoi(rbe) : 2;
+            const char *vm = getenv("DM_VOLUME_MINW");
+            if (NW1 == 4 && vm && vm[0] == '5') k_volume_cs<1, 2, 4, 4, true, 5><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 4 && vm && vm[0] == '6') k_volume_cs<1, 2, 4, 2, true, 6><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 4 && rb == 2) k_volume_cs<1, 2, 4, 2, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 4 && rb == 8) k_volume_cs<1, 2, 4, 8, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true><<<cgrid, 512, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true><<<cgrid, 128, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            else k_volume_cs<1, 2, 1, 4, true><<<cgrid, 64, 0, sc>>>(gc, s, Bw, QS, d_l0);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
         const int KS = (b->ws * b->ws + 63) / 64, GW = b->w0 / 16 / mfq_nw(b);
         const size_t waves = (size_t)b->T * (b->h0 / 4) * (b->w0 / 4);
         const unsigned vgrid = (unsigned)((waves + 3) / 4);

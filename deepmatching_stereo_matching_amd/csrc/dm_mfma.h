@@ -827,6 +827,181 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     }
 }
 
+// ===================================================================================
+// Level-0 volume, column-split (the k_level1_mfq workgroup shape): NW waves share 16
+// patches, wave w sweeps column group w.  Per-patch min/max are reduced through LDS once;
+// in sweep 2 the waves fill a shared LDS stage of RB rows x w0 windows x 16 patches and the
+// workgroup stores it as 16 contiguous runs of RB*w0*4 bytes (one per patch) with 16-B
+// non-temporal stores -- longer HBM write runs than one wave can stage alone.
+// ===================================================================================
+template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1>
+__global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+                                                       const int2 *__restrict__ QS, float *vol)
+{
+    constexpr int G = GW * NW, W0 = 16 * G; // w0 is a template constant here
+    __shared__ __attribute__((aligned(16))) float stage[16][RB][W0];
+    __shared__ float red[2][NW][16];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, grp = lane >> 4;
+    const int h0 = g.h0, n = g.ws * g.ws, P = h0 * W0;
+    const int nbj = W0 / 4, bpt = (h0 / 4) * nbj;
+    const int t = blockIdx.x / bpt;
+    const int I0 = 2 * ((blockIdx.x % bpt) / nbj), J0 = 2 * ((blockIdx.x % bpt) % nbj);
+    const size_t tb = (size_t)t * P;
+    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+
+    dm_v4i A[KS];
+    {
+        const int cl = c >> 2, ch = c & 3;
+        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
+        }
+    }
+    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
+    int sTr[4];
+    float sTf[4], ap[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+        sTr[r] = s.sT[tb + p];
+        sTf[r] = (float)sTr[r];
+        ap[r] = s.aP[tb + p];
+    }
+    const int ab = YF ? DM_YBIAS : 0;
+    const dm_v4i acc0 = {ab, ab, ab, ab};
+    const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
+    const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void *)Bt, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc((void *)Qt, 0, 0x7fffffff, 0x00020000);
+    const unsigned voB = (unsigned)lane * 16u, voQ = (unsigned)c * 8u;
+    struct RowFrag {
+        dm_v4i b[GW][KS];
+        int2 q[GW];
+    };
+    auto load_row = [&](RowFrag &f, int q0) {
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            const unsigned ti = (unsigned)q0 * G + tw;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                f.b[tw][ks] = __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (ti * KS + ks) * 1024u, 0);
+            const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
+            f.q[tw] = make_int2(qv.x, qv.y);
+        }
+    };
+
+    // ---- sweep 1: min / max of y over this wave's columns, then over the waves ----
+    float mn[4], mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
+    RowFrag fa, fb;
+    load_row(fa, 0);
+    for (int q0 = 0; q0 < h0; q0 += 2) {
+        load_row(fb, q0 + 1);
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
+        }
+        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        for (int off = 1; off < 16; off <<= 1) {
+            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
+            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        if (c == 0) { red[0][wave][4 * grp + r] = mn[r]; red[1][wave][4 * grp + r] = mx[r]; }
+    }
+    __syncthreads();
+    float lo[4], hi[4], rmn[4], den[4], rinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float a = red[0][0][4 * grp + r], b = red[1][0][4 * grp + r];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) { a = fminf(a, red[0][w][4 * grp + r]); b = fmaxf(b, red[1][w][4 * grp + r]); }
+        rmn[r] = r_of_y(a, ap[r], g.method);
+        const float rmx = r_of_y(b, ap[r], g.method);
+        den[r] = __fsub_rn(rmx, rmn[r]);
+        rinv[r] = __frcp_rn(den[r]);
+        const bool cc = g.method == DM_TM_CCOEFF;
+        lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
+        hi[r] = cc ? INFINITY : 1.0f;
+        if (wave == 0 && c == 0) {
+            const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+            s.rmn[tb + p] = rmn[r];
+            s.rmx[tb + p] = rmx;
+        }
+    }
+
+    // ---- sweep 2: x for this wave's columns -> stage; every RB rows the workgroup stores ----
+    typedef float fv __attribute__((ext_vector_type(GW)));
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    auto emit = [&](const RowFrag &f, int q0) {
+        float xs[GW][4];
+#pragma unroll
+        for (int tw = 0; tw < GW; ++tw) {
+            float y[4];
+            y_of_acc<YF>(mfma16_frag_c<KS>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);
+                xs[tw][r] = norm_mk(rr, rmn[r], den[r], rinv[r]);
+            }
+        }
+        const int col = 16 * GW * wave + GW * c, slot = q0 % RB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            fv v;
+#pragma unroll
+            for (int tw = 0; tw < GW; ++tw) v[tw] = xs[tw][r];
+            *(fv *)&stage[4 * grp + r][slot][col] = v;
+        }
+        if (slot == RB - 1) {
+            __syncthreads();
+            constexpr int PER = RB * W0 / 4;   // float4 per patch run
+            constexpr int TOT = 16 * PER;
+            const size_t pbase = tb + (size_t)(2 * I0) * W0 + 2 * J0;
+            const int qbase = (q0 - RB + 1) * W0;
+#pragma unroll
+            for (int i = tid; i < TOT; i += 64 * NW) {
+                const int pl = i / PER, k4 = i % PER;
+                const f4v v4 = *(const f4v *)(&stage[pl][0][0] + 4 * k4);
+                const int pc = pl >> 2, pch = pl & 3;
+                const size_t prow = pbase + (size_t)(2 * (pc >> 1) + (pch >> 1)) * W0 + 2 * (pc & 1) + (pch & 1);
+                __builtin_nontemporal_store(v4, (f4v *)(vol + prow * (size_t)P + qbase) + k4);
+            }
+            __syncthreads();
+        }
+    };
+    for (int q0 = 0; q0 < h0; q0 += 2) {
+        load_row(fb, q0 + 1);
+        emit(fa, q0);
+        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
+        emit(fb, q0 + 1);
+    }
+}
+
 static bool mf16_eligible(const dm_tiles *b)
 {
     // w0 in {32, 64, 128, 256}: the instantiated column-group counts G = w0/16 = 2, 4, 8, 16

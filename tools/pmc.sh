@@ -11,7 +11,7 @@ k=0
 for grp in "$@"; do
     k=$((k + 1))
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$k" -o run -- \
-        python3 "$REPO/tools/kbench.py" --variants "$VAR" --rounds 1 > "$OUT/p$k.log" 2>&1
+        python3 "$REPO/tools/${BENCH:-kbench}.py" --variants "$VAR" --rounds 1 > "$OUT/p$k.log" 2>&1
 done
 python3 "$REPO/tools/pmc_summary.py" "$OUT" > "$OUT/summary.txt"
 cat "$OUT/summary.txt"

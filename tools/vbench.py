@@ -1,0 +1,60 @@
+"""Volume-kernel A/B timer: dm_corr_volume on the C3 batch (or --tiles of it), variants as
+env settings ("cs", "cs+DM_VOLUME_RB=2", "mfq+DM_VOLUME_CS=0"), interleaved rounds.
+
+    python tools/vbench.py [--variants cs,mfq+DM_VOLUME_CS=0] [--rounds 3] [--tiles 32]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
+from deepmatching_stereo_matching_amd import engine  # noqa: E402
+from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
+
+KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--variants', default='cs')
+    ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--tile', type=int, default=128)
+    ap.add_argument('--tiles', type=int, default=32)
+    args = ap.parse_args()
+    S, ws = args.tile, 5
+    side = 9 * S + ws - 1
+    a, b = stereo_pair(side, side, seed=1000, dx=2, max_disp=S // 4, sinusoidal=True)
+    dev = torch.device('cuda', 0)
+    n, org = engine.cut_grid(a.shape, [S, S], [S, S], ws)
+    org = org[:args.tiles]
+    ia, ib = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    lib = L.load()
+    batch = engine.TileBatch(ia, ib, org, S, S, ws, L.DM_TM_CCOEFF_NORMED, dev)
+    pyr = engine.DevicePyramid(batch, build=False).compute_stats()
+    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=dev)
+    res = {v: [] for v in args.variants.split(',')}
+    for rnd in range(args.rounds + 1):
+        for v in res:
+            for k in KNOBS:
+                os.environ.pop(k, None)
+            for kv in v.split('+')[1:]:
+                k, val = kv.split('=')
+                os.environ[k] = val
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(lib.dm_corr_volume(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
+            e1.record()
+            torch.cuda.synchronize()
+            if rnd:
+                res[v].append(e0.elapsed_time(e1))
+    gb = 4.0 * vol.numel() / 1e9
+    for v, ts in res.items():
+        print('%-24s median %8.3f ms  %7.1f GB/s' % (v, np.median(ts), gb / (np.median(ts) * 1e-3)))
+
+
+if __name__ == '__main__':
+    main()
