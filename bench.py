@@ -61,23 +61,33 @@ class PairSolver:
     """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
     dominant kernel (dm_corr_level1)."""
 
-    def __init__(self, img1, img2, tile, grid):
+    def __init__(self, img1, img2, tile, grid, split=False):
+        """split: the pair's tiles are sharded over the ranks (rank r solves tiles r::N) and
+        the per-tile results are all-gathered before stitching (RCCL over xGMI); otherwise
+        this rank solves every tile of its own pair."""
+        from deepmatching_stereo_matching_amd import shard
         self.dev = img1.device
         self.tile = tile
-        self.n, self.origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
+        self.n, origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
         assert self.n == [grid, grid], self.n
+        self.rank, self.world = shard.world() if split else (0, 1)
+        self.T = len(origins)
+        self.origins = origins[shard.rank_units(self.T, self.rank, self.world)]
         self.batch = engine.TileBatch(img1, img2, self.origins, tile, tile, WS,
                                       L.DM_TM_CCOEFF_NORMED, self.dev)
         self.ev = []
 
     def step(self, timed=False):
+        from deepmatching_stereo_matching_amd import shard
         pyr = engine.DevicePyramid(self.batch, build=False)
         ev = None
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev.append(ev)
-        pyr.build(events=ev)               # stats, dm_corr_level1 [timed], dm_aggregate levels 2..
+        pyr.build(events=ev)               # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
         match = pyr.match(sub_pix=True)
+        if self.world > 1:
+            match = shard._gather_units(match, self.T, self.rank, self.world, match.shape[1:], match.dtype)
         dmap, score = engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                                     ['elevation'])
         return dmap, score
@@ -169,10 +179,14 @@ def main():
     # ImageCutSolver's floor rule (image_cut_solver.py:62): floor((side - (tile+ws-1)) / tile)
     # tiles per axis, so a grid x grid cut needs side = (grid+1)*tile + ws-1 (1156 for C3)
     side = (grid + 1) * tile + WS - 1
-    a, b = stereo_pair(side, side, seed=1000 + rank, dx=2, max_disp=tile // 4, sinusoidal=True)
+    # c5 (BASELINE configs[4]): ONE pair per step, its tiles sharded over the ranks (strong
+    # scaling, results all-gathered); c2/c3: one pair per rank per step (weak scaling)
+    split = args.config == 'c5' and world > 1
+    a, b = stereo_pair(side, side, seed=1000 + (0 if split else rank), dx=2, max_disp=tile // 4,
+                       sinusoidal=True)
     img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
-    solver = PairSolver(img1, img2, tile, grid)
-    voxels = solver.batch.T * float(tile) ** 4
+    solver = PairSolver(img1, img2, tile, grid, split=split)
+    voxels = solver.T * float(tile) ** 4      # per pair
 
     for _ in range(args.warmup):
         solver.step()
@@ -194,31 +208,34 @@ def main():
         elapsed = float(t.item())
 
     ms_step = elapsed / args.steps * 1e3
-    value = world * args.steps * voxels / elapsed / 1e9
+    pairs = 1 if split else world                 # pairs solved per step by the whole job
+    value = pairs * args.steps * voxels / elapsed / 1e9
     l1_ms = solver.level1_ms()
     if rank == 0:
         # dominant kernel: the fused level-0 -> level-1 (-> level-2) kernel.  Algorithmic bytes per
         # 4 B per level-0 voxel (the volume a materialising L0 kernel
         # writes); this kernel keeps level 0 on chip, so "achieved" is the HBM-equivalent
         # rate and "traffic" (PMC) the bytes it really moves.
-        gbs = 4.0 * voxels / (l1_ms * 1e-3) / 1e9
+        vox_launch = solver.batch.T * float(tile) ** 4   # this rank's tiles per launch
+        gbs = 4.0 * vox_launch / (l1_ms * 1e-3) / 1e9
         mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
         kname = 'dm_corr_level1 (k_level1_mfq)' if mode == 0 else 'dm_corr_level12 (k_level1_mfq, level 2 fused)'
         roof = {'kernel': kname, 'bound': 'hbm', 'ms': round(l1_ms, 3),
                 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(tile),
                 'algorithmic': '4 B/voxel x %d voxels per launch (level 0 never leaves the chip)'
-                               % int(voxels)}
+                               % int(vox_launch)}
         rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
                'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
-               'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
+               'scaling': 'strong' if split else 'weak', 'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
                'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
                'config': {'workload': '%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
                                       '+ sub-pixel + cal_map + stitch'
                                       % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS),
                           'tile': tile, 'tiles_per_pair': grid * grid, 'window_size': WS,
-                          'pairs_per_gpu_per_step': 1, 'parallelism': 'pairs sharded %d-way' % world},
+                          'pairs_per_gpu_per_step': (1.0 / world) if split else 1,
+                          'parallelism': ('tiles of one pair sharded %d-way' if split else 'pairs sharded %d-way') % world},
                'roofline': roof}
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)
