@@ -215,7 +215,7 @@ def test_shape_errors_like_reference(mirror):
 
 @pytest.mark.parametrize('h0,w0,ws', [(32, 32, 5), (64, 64, 5), (128, 128, 5), (16, 64, 3),
                                       (32, 128, 7), (64, 64, 15), (128, 256, 5), (64, 128, 9)])
-def test_fused_level2_equals_aggregate(h0, w0, ws):
+def test_fused_level2_equals_aggregate(h0, w0, ws, method=5):
     """dm_corr_level12 (level 2 fused into the level-1 kernel, level 1 optionally written)
     equals dm_corr_level1 + dm_aggregate bit for bit; matching with level 1 evaluated on
     demand equals matching on the materialised level 1."""
@@ -224,9 +224,9 @@ def test_fused_level2_equals_aggregate(h0, w0, ws):
     from deepmatching_stereo_matching_amd.synthetic import stereo_pair
     a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=7 * h0 + w0 + ws, dx=3)
     org = [(0, 0), (4, 8), (2, 3)]
-    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=0)
-    fused = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=2)
-    both = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=1)
+    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, method), fuse_level2=0)
+    fused = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, method), fuse_level2=2)
+    both = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, method), fuse_level2=1)
     assert fused.levels[1] is None and ref.levels[1] is not None
     _same(both.levels[1].cpu().numpy(), ref.levels[1].cpu().numpy())
     _same(both.match().cpu().numpy(), ref.match().cpu().numpy())
@@ -244,6 +244,24 @@ def test_fused_level2_equals_aggregate(h0, w0, ws):
     _same(l1.cpu().numpy(), ref.levels[1].cpu().numpy())
     _same(l2.cpu().numpy(), ref.levels[2].cpu().numpy())
     _same(fused.level(1).cpu().numpy(), ref.levels[1].cpu().numpy())
+
+
+@pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (32, 128, 7)])
+def test_fused_level2_ccoeff_and_flat_patches(h0, w0, ws):
+    """The fused path with cv2.TM_CCOEFF, and with constant patches (NaN child maps)."""
+    test_fused_level2_equals_aggregate(h0, w0, ws, method=4)
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=h0 + 3 * ws, dx=2)
+    a[10:10 + ws + 3, 20:20 + ws + 5] = 200        # constant patches -> NaN maps (NORMED)
+    org = [(0, 0), (4, 8)]
+    res = []
+    for mode in (0, 2):
+        pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=mode)
+        res.append((pyr.levels[2].cpu().numpy(), pyr.match().cpu().numpy()))
+    assert np.isnan(res[0][0]).any()
+    _same(res[0][0], res[1][0])
+    _same(res[0][1], res[1][1])
 
 
 def test_fused_level2_unsupported_shapes():
