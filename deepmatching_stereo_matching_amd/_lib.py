@@ -15,7 +15,7 @@ import re
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libdmstereo.so')
+LIB_PATH = os.environ.get('DM_LIB_PATH') or os.path.join(HERE, 'libdmstereo.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'dmstereo.h')
 
 DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3, -4
