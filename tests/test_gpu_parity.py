@@ -179,6 +179,26 @@ def test_synthetic_tile_vs_oracle(S, ws, seed, mirror):
     _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
 
 
+@pytest.mark.parametrize('h0,w0,ws,method', [(8, 24, 3, 5), (16, 48, 5, 4), (32, 96, 5, 5), (64, 32, 7, 5),
+                                             (16, 16, 1, 5), (4, 4, 3, 5), (32, 64, 13, 4), (128, 64, 5, 5)])
+def test_shapes_vs_oracle(h0, w0, ws, method, mirror):
+    """Shapes across the generic (w0 not a power of two, small tiles) and MFMA paths, both
+    methods, window sizes 1..13: every level and the matching, bit for bit."""
+    CM, MT, CD = mirror
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1, w0 + ws - 1, seed=h0 * 7 + w0 + ws, dx=1)
+    feat = 'cv2.TM_CCOEFF_NORMED' if method == 5 else 'cv2.TM_CCOEFF'
+    co = CM.Correlation_map(a, b, window_size=ws, feature_name=feat)
+    co()
+    ol0 = O.corr_l0(a, b, ws, feat)
+    olev, it, _ = O.pyramid(ol0)
+    assert co.iteration == it
+    for k in range(1, len(olev)):
+        _same(co.co_map_list[k], olev[k])
+    if len(olev) > 1:
+        _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
+
+
 def test_batched_tiles_equal_single_tiles():
     """Batch invariance (size-independent property): one batched solve of a tile grid ==
     solving every tile alone; and the stitched map == per-tile cal_map."""
