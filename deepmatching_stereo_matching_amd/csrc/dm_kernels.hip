@@ -902,6 +902,17 @@ static int level1_variant(const dm_tiles *b)
     return 3; // column-split k_level1_mfq
 }
 
+// bf16 MFMA operands for the column-split kernels (exact for ws <= 5: K = 32 >= n, integer
+// accumulators < 2^24, so no bias trick is needed).  Opt-in (DM_MFMA_BF16=1): on C3 it
+// measured even with the i8 MFMA (the kernels are not VALU-issue bound after the bias add
+// goes).  dm_corr_stats lays the window operands out accordingly; every consumer
+// re-derives the same decision.
+static bool mfma_bf16(const dm_tiles *b)
+{
+    const char *e = getenv("DM_MFMA_BF16");
+    return level1_variant(b) == 3 && b->ws <= 5 && e && e[0] == '1';
+}
+
 // waves per workgroup of k_level1_mfq: NW = min(4, G/2); column group width GW = G/NW
 static int mfq_nw(const dm_tiles *b)
 {
@@ -1033,7 +1044,7 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
-template <bool L2F, bool YF>
+template <bool L2F, bool YF, bool BF = false>
 static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
                         hipStream_t st)
 {
@@ -1042,14 +1053,14 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     const Geo gg = make_geo(b);
     const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 4, 5 or 6 waves/SIMD
     if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] >= '4' && mw[0] <= '6') {
-        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 2, 4, 6, L2F, YF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 2, 4, 6, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
     // register budget: 5 waves/SIMD (measured best for both variants on C3)
-#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4) DM_MQ(1, 2, 8)
     if constexpr (!YF) {
         DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4) DM_MQ(2, 2, 8)
@@ -1069,6 +1080,7 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
     mfma_views(b, d_stats, &Bw, &QS);
     const Stats s = stats_view(d_stats, b->T, b->h0 * b->w0);
     const char *yf = getenv("DM_MFQ_YF");
+    if (mfma_bf16(b)) return launch_mfq_t<L2F, true, true>(b, s, Bw, QS, L1, L2, st);
     if (b->ws <= 5 && !(yf && yf[0] == '0')) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st);
     return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st);
 }
@@ -1105,7 +1117,8 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
         const size_t n = (size_t)b->T * b->h0 * G * 16;
         const int GW = var == 3 ? G / mfq_nw(b) : G;
-        k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
+        k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS,
+                                                                          mfma_bf16(b) ? 1 : 0);
         HIP_TRY(hipGetLastError());
     }
     return DM_OK;
@@ -1190,6 +1203,7 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         mfma_views(b, d_stats, &Bw, &QS);
         const char *cs = getenv("DM_VOLUME_CS");
         const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
+        const bool bf = mfma_bf16(b);
         if (!(cs && cs[0] == '0') && b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
             // column-split workgroups with a shared LDS stage (RB rows per store burst)
             const unsigned cgrid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
@@ -1198,6 +1212,14 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
             const char *rbe = getenv("DM_VOLUME_RB"); // A/B knob: rows per store burst (C3 shape)
             const int rb = rbe ? atoi(rbe) : 2;
             const char *vm = getenv("DM_VOLUME_MINW");
+            if (bf) {
+                if (NW1 == 4) k_volume_cs<1, 2, 4, 2, true, 1, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
+                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, true><<<cgrid, 512, 0, sc>>>(gc, s, Bw, QS, d_l0);
+                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, true><<<cgrid, 128, 0, sc>>>(gc, s, Bw, QS, d_l0);
+                else k_volume_cs<1, 2, 1, 4, true, 1, true><<<cgrid, 64, 0, sc>>>(gc, s, Bw, QS, d_l0);
+                HIP_TRY(hipGetLastError());
+                return DM_OK;
+            }
             if (NW1 == 4 && vm && vm[0] == '5') k_volume_cs<1, 2, 4, 4, true, 5><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
             else if (NW1 == 4 && vm && vm[0] == '6') k_volume_cs<1, 2, 4, 2, true, 6><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
             else if (NW1 == 4 && rb == 2) k_volume_cs<1, 2, 4, 2, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
@@ -1218,6 +1240,13 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         const bool yf = b->ws <= 5;
         const Geo gg = make_geo(b);
         hipStream_t st = (hipStream_t)stream;
+        if (bf) { // window operands are bf16 (KS = 1, GW = 2 or 4)
+            if (GW == 2 && lds) k_volume_mfq<1, 2, true, true, true, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
+            else if (GW == 2) k_volume_mfq<1, 2, true, true, false, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
+            else k_volume_mfq<1, 4, true, true, false, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
 #define DM_VQ(KS_, GW_, YF_, NT_, LS_) if (KS == KS_ && GW == GW_ && yf == YF_ && ntst == NT_ && lds == LS_) { k_volume_mfq<KS_, GW_, YF_, NT_, LS_><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0); HIP_TRY(hipGetLastError()); return DM_OK; }
         DM_VQ(1, 2, true, true, true) DM_VQ(1, 2, true, true, false) DM_VQ(1, 2, true, false, true) DM_VQ(1, 2, true, false, false)
         DM_VQ(1, 4, true, true, false) DM_VQ(1, 4, true, false, false)

@@ -33,7 +33,7 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 // Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
 // lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
 // GW = G/NW: one group per wave of k_level1_mfq.
-__global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS)
+__global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS, int bf)
 {
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t total = (size_t)g.T * g.h0 * G * 16;
@@ -57,6 +57,20 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
     else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
     QS[idx] = make_int2(__float_as_int((float)-s), __float_as_int(bq)); // exact: |s| <= 225*128
     const size_t tile = idx / 16; // (t, q0, tau)
+    if (bf) { // bf16 operands (v_mfma_f32_16x16x32_bf16, K = 32 >= n): lane c+16hq, taps 8hq..8hq+7
+        for (int hq = 0; hq < 4; ++hq) {
+            int w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * hq + j;
+                const int val = k < n ? (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128 : 0;
+                w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1))); // exact in bf16
+            }
+            dm_v4i o;
+            o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
+            Bw[tile * 64 + c + 16 * hq] = o;
+        }
+        return;
+    }
     for (int ks = 0; ks < KS; ++ks)
         for (int hq = 0; hq < 4; ++hq) {
             int w[4] = {0, 0, 0, 0};
@@ -108,16 +122,17 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
 #define DM_YBIAS 0x4B400000
 typedef float dm_f2 __attribute__((ext_vector_type(2)));
 
-template <bool YF>
+template <bool YF, bool BF = false>
 __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, const float *sTf, int2 qs, int n,
                                          float *y)
 {
     const float b = __int_as_float(qs.y);
     if constexpr (YF) {
         const float nf = (float)n, sI = __int_as_float(qs.x);
-        const dm_f2 bias = {12582912.0f, 12582912.0f};
-        const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])} - bias;
-        const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])} - bias;
+        const dm_f2 bias = BF ? dm_f2{0.0f, 0.0f} : dm_f2{12582912.0f, 12582912.0f};
+        dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
+        dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
+        if constexpr (!BF) { a01 = a01 - bias; a23 = a23 - bias; }
         const dm_f2 p01 = dm_f2{sTf[0], sTf[1]} * dm_f2{sI, sI};
         const dm_f2 p23 = dm_f2{sTf[2], sTf[3]} * dm_f2{sI, sI};
         const dm_f2 n01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, p01);
@@ -128,6 +143,36 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
+    }
+}
+
+// A operand of one lane: patch rows of a 2x2 cell block (row c: cell cl = c/4, child ch = c%4),
+// int8 taps 64ks + 16grp + j (i8 MFMA) or bf16 taps 8grp + j (BF, KS = 1)
+template <int KS, bool BF>
+__device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, int J0, int c, int grp)
+{
+    const int n = g.ws * g.ws;
+    const int cl = c >> 2, ch = c & 3;
+    const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+    const uint8_t *base = g.img1 + (size_t)(g.org[2 * t] + p0) * g.pitch1 + g.org[2 * t + 1] + p1;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        int w[4] = {0, 0, 0, 0};
+        if constexpr (BF) {
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * grp + j;
+                const int val = k < n ? (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128 : 0;
+                w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1)));
+            }
+        } else {
+            for (int j = 0; j < 16; ++j) {
+                const int k = 64 * ks + 16 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
+        }
+        A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
     }
 }
 
@@ -149,6 +194,23 @@ __device__ __forceinline__ float dpp_prev16(float v)
 __device__ __forceinline__ float dpp_prev16_or(float v, float old)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+
+// one 16x16 tile: i8 MFMA onto acc0 (YF bias) or, BF, the bf16 MFMA whose f32 accumulator
+// is exact (integer partial sums < 2^24) -- returned as raw bits either way
+template <int KS, bool BF>
+__device__ __forceinline__ dm_v4i mfma_tile(const dm_v4i *A, const dm_v4i *Bf, dm_v4i acc0)
+{
+    if constexpr (BF) {
+        typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        v4f c = {0.0f, 0.0f, 0.0f, 0.0f};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, A[0]), __builtin_bit_cast(v8bf, Bf[0]),
+                                                     c, 0, 0, 0);
+        return __builtin_bit_cast(dm_v4i, c);
+    } else {
+        return mfma16_frag_c<KS>(A, Bf, acc0);
+    }
 }
 
 __device__ __forceinline__ float shfl_prev16(float v, int lane)
@@ -340,7 +402,7 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
 __device__ __forceinline__ double nanmax_d(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
 
 // L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
-template <int KS, int GW, int NW, int MINW, bool L2F, bool YF>
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
@@ -374,22 +436,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    {
-        const int cl = c >> 2, ch = c & 3;
-        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
-        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 64 * ks + 16 * grp + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
-        }
-    }
+    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
     float sTf[4];
@@ -435,9 +482,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto minmax_row = [&](const RowFrag &f) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma16_frag_c<KS>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF>(acc, sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 mn[r] = fminf(mn[r], y[r]);
@@ -507,9 +554,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&last)[4]) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma16_frag_c<KS>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF>(acc, sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if ((tw & 1) == 0) Cm[tw / 2][r] = tw == 0 ? y[r] : fmaxf(last[r], y[r]);
@@ -653,7 +700,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 // lane c's GW tiles of group g are GW consecutive floats: one GW-float vector store per
 // patch, a 16-lane group writing 64*GW/... = 16*GW*4 contiguous bytes of the patch's row.
 // ===================================================================================
-template <int KS, int GW, bool YF, bool NT, bool LS>
+template <int KS, int GW, bool YF, bool NT, bool LS, bool BF = false>
 __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                     const int2 *__restrict__ QS, float *vol)
 {
@@ -673,22 +720,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    {
-        const int cl = c >> 2, ch = c & 3;
-        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
-        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 64 * ks + 16 * grp + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
-        }
-    }
+    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4], pr[4];
     float sTf[4], ap[4];
@@ -735,7 +767,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -743,7 +775,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -777,7 +809,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);
@@ -834,7 +866,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // workgroup stores it as 16 contiguous runs of RB*w0*4 bytes (one per patch) with 16-B
 // non-temporal stores -- longer HBM write runs than one wave can stage alone.
 // ===================================================================================
-template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1>
+template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1, bool BF = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                        const int2 *__restrict__ QS, float *vol)
 {
@@ -852,22 +884,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    {
-        const int cl = c >> 2, ch = c & 3;
-        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
-        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 64 * ks + 16 * grp + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
-        }
-    }
+    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
     float sTf[4], ap[4];
@@ -912,7 +929,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -920,7 +937,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -962,7 +979,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF>(mfma16_frag_c<KS>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);

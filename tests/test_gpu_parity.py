@@ -199,6 +199,25 @@ def test_shapes_vs_oracle(h0, w0, ws, method, mirror):
         _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
 
 
+@pytest.mark.parametrize('S,ws', [(64, 5), (128, 3), (32, 5)])
+def test_bf16_operands_equal_i8(S, ws, monkeypatch):
+    """The bf16-MFMA operand path (DM_MFMA_BF16=1) gives the i8-MFMA results bit for bit:
+    levels, matching, the level-0 volume."""
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(S + ws - 1 + 6, S + ws - 1 + 6, seed=S + ws, dx=2)
+    org = [(0, 0), (3, 5)]
+    res = {}
+    for bf in ('0', '1'):
+        monkeypatch.setenv('DM_MFMA_BF16', bf)
+        pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, ws, 5))
+        res[bf] = [pyr.levels[k].cpu().numpy() for k in range(2, pyr.nlev)] + \
+                  [pyr.match().cpu().numpy(), pyr.volume().cpu().numpy()]
+        del pyr
+    for x, y in zip(res['0'], res['1']):
+        _same(x, y)
+
+
 def test_batched_tiles_equal_single_tiles():
     """Batch invariance (size-independent property): one batched solve of a tile grid ==
     solving every tile alone; and the stitched map == per-tile cal_map."""
