@@ -147,18 +147,23 @@ def cpu_baseline(tiles, tile):
                       '(OpenMP), %.2f s' % (tiles, tile, vox / 1e9, dt)}
 
 
-def load_traffic(tile, kernel='level1'):
-    """HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) of a kernel from
-    the committed rocprofv3 PMC passes (profiles/pmc_<kernel>.json, tools/profile.sh)."""
+def load_pmc(tile, kernel='level1'):
+    """Per-launch PMC figures of a kernel from the committed rocprofv3 passes
+    (profiles/pmc_<kernel>.json, tools/profile.sh): HBM bytes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE) and, for the level kernel, VALU instructions."""
     path = os.path.join(REPO, 'profiles', 'pmc_%s.json' % kernel)
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get('tile') == tile:
-            return d.get('hbm_bytes_per_launch')
+            return d
     except (OSError, ValueError):
         pass
-    return None
+    return {}
+
+
+def load_traffic(tile, kernel='level1'):
+    return load_pmc(tile, kernel).get('hbm_bytes_per_launch')
 
 
 def main():
@@ -225,6 +230,11 @@ def main():
                 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(tile),
                 'algorithmic': '4 B/voxel x %d voxels per launch (level 0 never leaves the chip)'
                                % int(vox_launch)}
+        # what actually bounds it: VALU issue (f64 pow + f32 normalisation), from the PMC
+        # VALU instruction count: wave64 VALU op = 4 cycles on a SIMD, 1024 SIMDs, 2.4 GHz
+        valu = load_pmc(tile).get('valu_insts_per_launch') if world == 1 else None
+        if valu:
+            roof['valu_issue_frac'] = round(valu * 4.0 / (1024 * l1_ms * 1e-3 * 2.4e9), 3)
         rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
                'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,

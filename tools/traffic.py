@@ -25,6 +25,11 @@ def main(root, tile):
         d = {'kernel': prefix, 'tile': tile, 'fetch_kib': f, 'write_kib': w,
              'hbm_bytes_per_launch': int(2 * f * 1024 + w * 1024),
              'note': 'FETCH_SIZE x2 (gfx950) + WRITE_SIZE, mean over the launches of bench.py'}
+        sq = os.path.join(root, 'sq', 'run_counter_collection.csv')
+        if key == 'level1' and os.path.exists(sq):
+            v = per_launch(sq, 'SQ_INSTS_VALU', prefix)
+            if v is not None:
+                d['valu_insts_per_launch'] = v
         with open(os.path.join(root, 'pmc_%s.json' % key), 'w') as fh:
             json.dump(d, fh, indent=1)
         print(json.dumps(d))
