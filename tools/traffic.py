@@ -6,7 +6,7 @@ import json
 import os
 import sys
 
-KERNELS = {'level1': 'k_level1_mfq', 'volume': 'k_volume_mfq'}
+KERNELS = {'level1': ('k_level1_mfq',), 'volume': ('k_volume_cs', 'k_volume_mfq')}
 
 
 def per_launch(path, counter, prefix):
@@ -17,9 +17,12 @@ def per_launch(path, counter, prefix):
 
 
 def main(root, tile):
-    for key, prefix in KERNELS.items():
-        f = per_launch(os.path.join(root, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE', prefix)
-        w = per_launch(os.path.join(root, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE', prefix)
+    for key, prefixes in KERNELS.items():
+        for prefix in prefixes:
+            f = per_launch(os.path.join(root, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE', prefix)
+            w = per_launch(os.path.join(root, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE', prefix)
+            if f is not None and w is not None:
+                break
         if f is None or w is None:
             continue
         d = {'kernel': prefix, 'tile': tile, 'fetch_kib': f, 'write_kib': w,
