@@ -13,8 +13,9 @@ synchronize bracketed, max over ranks.
 
 Also reported: the roofline of the dominant kernel (dm_corr_level1), timed with HIP
 events on the launch stream inside the timed steps, the HBM roofline of the level-0
-volume kernel (dm_corr_volume, 4 B/voxel written) on the same batch, and the CPU oracle's
-rate on a bounded sample (rank 0, N=1).
+volume kernel (dm_corr_volume, 4 B/voxel written, and its fp16 variant, 2 B/voxel) on the
+same batch, the fp16 volume's argmax flip rate, and the CPU oracle's rate on a bounded
+sample (rank 0, N=1).
 """
 
 import argparse
@@ -96,34 +97,63 @@ class PairSolver:
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
 
 
-def volume_roofline(solver, reps=3):
-    """HBM roofline of the level-0 volume kernel (dm_corr_volume: co_map, float32, written in
-    full) on the same C3 batch: 4 B per voxel written."""
+def volume_roofline(solver, reps=3, f16=False):
+    """HBM roofline of the level-0 volume kernel on the same batch: dm_corr_volume (co_map,
+    float32, 4 B per voxel written) or, with f16, the fp16 volume of
+    BASELINE config C5 (dm_corr_volume_f16, 2 B per voxel written)."""
     full = solver.batch
-    nt = max(1, min(full.T, int(VOLUME_BUDGET // (4.0 * full.P * full.P))))
+    esz = 2 if f16 else 4
+    nt = max(1, min(full.T, int(VOLUME_BUDGET // (float(esz) * full.P * full.P))))
     batch = engine.TileBatch(full.img1, full.img2, full.origins_host[:nt], full.h0, full.w0, full.ws,
                              full.method, full.device)
     pyr = engine.DevicePyramid(batch, build=False)
     pyr.compute_stats()
-    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=batch.device)
+    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float16 if f16 else torch.float32,
+                      device=batch.device)
+    fn = pyr.lib.dm_corr_volume_f16 if f16 else pyr.lib.dm_corr_volume
     ts = []
     for i in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        L.check(pyr.lib.dm_corr_volume(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
+        L.check(fn(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
         e1.record()
         torch.cuda.synchronize()
         if i:
             ts.append(e0.elapsed_time(e1))
     ms = float(np.mean(ts))
     voxels = batch.T * batch.P * batch.P
-    gbs = 4.0 * voxels / (ms * 1e-3) / 1e9
+    gbs = esz * voxels / (ms * 1e-3) / 1e9
     del vol, pyr
     torch.cuda.empty_cache()
-    return {'kernel': 'dm_corr_volume (k_volume_mfq)', 'tiles': batch.T, 'tile': batch.h0,
-            'ms': round(ms, 3), 'algorithmic_bytes_per_voxel': 4, 'bound': 'hbm',
+    name = 'dm_corr_volume_f16 (k_volume_cs, binary16)' if f16 else 'dm_corr_volume (k_volume_cs)'
+    return {'kernel': name, 'tiles': batch.T, 'tile': batch.h0,
+            'ms': round(ms, 3), 'gvox_s': round(voxels / (ms * 1e-3) / 1e9, 1),
+            'algorithmic_bytes_per_voxel': esz, 'bound': 'hbm',
             'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(batch.h0, 'volume')}
+            'frac': round(gbs / HBM_PEAK_GBS, 4),
+            'traffic': load_traffic(batch.h0, 'volume_f16' if f16 else 'volume')}
+
+
+def fp16_flip_rate(solver, tiles=2):
+    """Argmax flip rate of the fp16-volume pyramid (dm_corr_volume_f16 -> rectify ->
+    aggregate -> match) against the float32 path on `tiles` tiles of the workload: the
+    fraction of pixels whose integer correspondence differs (C5 fp16 has no
+    bit-exact claim, its flip rate is reported)."""
+    full = solver.batch
+    flips, n = 0, 0
+    for t in range(min(tiles, full.T)):   # one tile at a time: its float64 level 0 is 8 B/voxel
+        one = engine.TileBatch(full.img1, full.img2, full.origins_host[t:t + 1], full.h0, full.w0,
+                               full.ws, full.method, full.device)
+        pyr = engine.DevicePyramid(one)
+        ref = pyr.match(sub_pix=False)
+        lv = pyr.materialized_levels('f16')
+        m16 = pyr.match(sub_pix=False, levels=lv)
+        flips += int((m16[:, :2] != ref[:, :2]).any(dim=1).sum())
+        n += one.P
+        del lv, pyr
+        torch.cuda.empty_cache()
+    return {'tiles': tiles, 'tile': full.h0, 'pixels': n, 'flipped': flips,
+            'rate': round(flips / n, 6)}
 
 
 def cpu_baseline(tiles, tile):
@@ -249,6 +279,9 @@ def main():
                'roofline': roof}
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)
+            rec['volume_f16_kernel_roofline'] = volume_roofline(solver, f16=True)
+            if world == 1:
+                rec['fp16_flip_rate'] = fp16_flip_rate(solver)
         if world == 1 and not args.no_cpu_baseline and tile <= 128:   # S=256: 17 GB level 0 per tile on the host
             rec['cpu_baseline'] = cpu_baseline(args.cpu_sample_tiles, tile)
         print(json.dumps(rec))

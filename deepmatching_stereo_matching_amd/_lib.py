@@ -51,6 +51,8 @@ SIGNATURES = {
     'dm_corr_level1': ([_TP, _P, _P, _P], ctypes.c_int),
     'dm_corr_level12': ([_TP, _P, _P, _P, _P], ctypes.c_int),
     'dm_corr_volume': ([_TP, _P, _P, _P], ctypes.c_int),
+    'dm_corr_volume_f16': ([_TP, _P, _P, _P], ctypes.c_int),
+    'dm_rectify_f16': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify64': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_aggregate': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),

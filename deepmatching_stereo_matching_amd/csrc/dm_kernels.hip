@@ -410,17 +410,18 @@ __global__ __launch_bounds__(256) void k_minmax(Geo g, Stats s)
     }
 }
 
-__global__ __launch_bounds__(256) void k_volume(Geo g, Stats s, float *l0)
+template <typename OT>
+__global__ __launch_bounds__(256) void k_volume(Geo g, Stats s, OT *l0)
 {
     const int P = g.h0 * g.w0, t = blockIdx.y, p = blockIdx.x;
     const int p0 = p / g.w0, p1 = p % g.w0;
     const size_t tb = (size_t)t * P;
     const int sT = s.sT[tb + p];
     const float ap = s.aP[tb + p], mn = s.rmn[tb + p], mx = s.rmx[tb + p];
-    float *row = l0 + (tb + p) * P;
+    OT *row = l0 + (tb + p) * P;
     for (int q = threadIdx.x; q < P; q += 256) {
         const float y = y_of_num(num_global(g, t, p0, p1, q / g.w0, q % g.w0, sT, s.sI[tb + q]), s.bQ[tb + q]);
-        row[q] = norm_x(r_of_y(y, ap, g.method), mn, mx);
+        row[q] = (OT)norm_x(r_of_y(y, ap, g.method), mn, mx);
     }
 }
 
@@ -1087,7 +1088,7 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 
 extern "C" {
 
-int dm_abi_version(void) { return 101; }
+int dm_abi_version(void) { return 102; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1256,7 +1257,59 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
     }
     k_minmax<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s);
     HIP_TRY(hipGetLastError());
-    k_volume<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s, d_l0);
+    k_volume<float><<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s, d_l0);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats || !d_l0) return fail(DM_ERR_ARG, "null workspace / output");
+    const int P = b->h0 * b->w0;
+    Stats s = stats_view(d_stats, b->T, P);
+    _Float16 *out = (_Float16 *)d_l0;
+    hipStream_t st = (hipStream_t)stream;
+    if (level1_variant(b) == 3) {
+        dm_v4i *Bw;
+        int2 *QS;
+        mfma_views(b, d_stats, &Bw, &QS);
+        const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
+        if (b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
+            // the float32 column-split kernel with a binary16 stage: 4 rows per store burst
+            // keep the per-patch runs at RB*w0*2 = 1 KB (C3 shape)
+            const unsigned cgrid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
+            const Geo gc = make_geo(b);
+            if (mfma_bf16(b)) {
+                if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, true, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, true, _Float16><<<cgrid, 512, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, true, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
+                else k_volume_cs<1, 2, 1, 4, true, 1, true, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);
+            } else {
+                if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, false, _Float16><<<cgrid, 512, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, false, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
+                else k_volume_cs<1, 2, 1, 4, true, 1, false, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);
+            }
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+    }
+    dim3 grid(P, b->T);
+    k_minmax<<<grid, 256, 0, st>>>(make_geo(b), s);
+    HIP_TRY(hipGetLastError());
+    k_volume<_Float16><<<grid, 256, 0, st>>>(make_geo(b), s, out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_rectify_f16(const uint16_t *d_in, size_t n, double *d_out, void *stream)
+{
+    if (!d_in || !d_out) return fail(DM_ERR_ARG, "null pointer");
+    if (n == 0) return DM_OK;
+    k_rectify<_Float16><<<nblk(n, 256) > 8192 ? 8192 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(
+        (const _Float16 *)d_in, n, d_out);
     HIP_TRY(hipGetLastError());
     return DM_OK;
 }

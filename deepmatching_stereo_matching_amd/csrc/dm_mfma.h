@@ -866,12 +866,15 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // workgroup stores it as 16 contiguous runs of RB*w0*4 bytes (one per patch) with 16-B
 // non-temporal stores -- longer HBM write runs than one wave can stage alone.
 // ===================================================================================
-template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1, bool BF = false>
+// OT = float (co_map, 4 B/voxel) or _Float16 (the fp16 volume of BASELINE config C5,
+// 2 B/voxel: the float32 value rounded to nearest-even binary16, as np.float16(co_map)).
+template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1, bool BF = false, typename OT = float>
 __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                       const int2 *__restrict__ QS, float *vol)
+                                                       const int2 *__restrict__ QS, OT *vol)
 {
     constexpr int G = GW * NW, W0 = 16 * G; // w0 is a template constant here
-    __shared__ __attribute__((aligned(16))) float stage[16][RB][W0];
+    constexpr int EV = 16 / sizeof(OT);     // elements per 16-B store
+    __shared__ __attribute__((aligned(16))) OT stage[16][RB][W0];
     __shared__ float red[2][NW][16];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -972,8 +975,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
     }
 
     // ---- sweep 2: x for this wave's columns -> stage; every RB rows the workgroup stores ----
-    typedef float fv __attribute__((ext_vector_type(GW)));
-    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef OT fv __attribute__((ext_vector_type(GW)));
+    typedef OT f4v __attribute__((ext_vector_type(EV)));
     auto emit = [&](const RowFrag &f, int q0) {
         float xs[GW][4];
 #pragma unroll
@@ -991,19 +994,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
         for (int r = 0; r < 4; ++r) {
             fv v;
 #pragma unroll
-            for (int tw = 0; tw < GW; ++tw) v[tw] = xs[tw][r];
+            for (int tw = 0; tw < GW; ++tw) v[tw] = (OT)xs[tw][r];
             *(fv *)&stage[4 * grp + r][slot][col] = v;
         }
         if (slot == RB - 1) {
             __syncthreads();
-            constexpr int PER = RB * W0 / 4;   // float4 per patch run
+            constexpr int PER = RB * W0 / EV;  // 16-B vectors per patch run
             constexpr int TOT = 16 * PER;
             const size_t pbase = tb + (size_t)(2 * I0) * W0 + 2 * J0;
             const int qbase = (q0 - RB + 1) * W0;
 #pragma unroll
             for (int i = tid; i < TOT; i += 64 * NW) {
                 const int pl = i / PER, k4 = i % PER;
-                const f4v v4 = *(const f4v *)(&stage[pl][0][0] + 4 * k4);
+                const f4v v4 = *(const f4v *)(&stage[pl][0][0] + EV * k4);
                 const int pc = pl >> 2, pch = pl & 3;
                 const size_t prow = pbase + (size_t)(2 * (pc >> 1) + (pch >> 1)) * W0 + 2 * (pc & 1) + (pch & 1);
                 __builtin_nontemporal_store(v4, (f4v *)(vol + prow * (size_t)P + qbase) + k4);

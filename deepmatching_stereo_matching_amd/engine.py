@@ -183,6 +183,41 @@ class DevicePyramid:
             self._volume = v
         return self._volume
 
+    def volume_f16(self):
+        """The level-0 min-max volume as binary16 (dm_corr_volume_f16, BASELINE config C5's
+        fp16 correlation): float16 [T][P][P], each value np.float16 of volume()'s."""
+        self.compute_stats()
+        b = self.b
+        v = torch.empty((b.T, b.P, b.P), dtype=torch.float16, device=b.device)
+        L.check(self.lib.dm_corr_volume_f16(b.ref(), L.ptr(self.stats), L.ptr(v), self._s()),
+                'dm_corr_volume_f16')
+        self._have_minmax = True
+        return v
+
+    def materialized_levels(self, l0_dtype='f32'):
+        """co_map_list built the reference's way (misc/Correlation_map.py:132-156): level 0
+        stored (float32 ``co_map`` or its fp16 rounding), rectified to float64
+        (_rectification, :158-159), then every level by dm_aggregate (_aggregation,
+        :89-130).  With 'f32' the levels equal the fused path's bit for bit; 'f16' is the
+        C5 fp16-volume variant whose argmax flip rate the tests and bench report.
+        Needs T * P^2 * (8 + 2|4) bytes of HBM."""
+        b, lib = self.b, self.lib
+        v = self.volume_f16() if l0_dtype == 'f16' else self.volume()
+        l0 = torch.empty(v.shape, dtype=torch.float64, device=v.device)
+        fn = lib.dm_rectify_f16 if l0_dtype == 'f16' else lib.dm_rectify
+        L.check(fn(L.ptr(v), v.numel(), L.ptr(l0), self._s()), 'dm_rectify')
+        if l0_dtype == 'f16':
+            del v
+        levels, h, w = [l0], b.h0, b.w0
+        for _ in range(1, self.nlev):
+            P2 = (h // 2) * (w // 2)
+            nxt = torch.empty((b.T, P2, P2), dtype=torch.float64, device=b.device)
+            L.check(lib.dm_aggregate(L.ptr(levels[-1]), b.T, h, w, 1, L.ptr(nxt), self._s()),
+                    'dm_aggregate')
+            levels.append(nxt)
+            h, w = h // 2, w // 2
+        return levels
+
     def level(self, k):
         """co_map_list[k] as a float64 device tensor [T][Pk][Pk]."""
         if k < 0:
@@ -199,15 +234,20 @@ class DevicePyramid:
         return out
 
     def match(self, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
-              filtering_mode='median'):
-        """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score)."""
+              filtering_mode='median', levels=None):
+        """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score).
+        ``levels``: an explicit co_map_list (e.g. materialized_levels()) to match on
+        instead of this pyramid's (level 0 then read from memory, not re-derived)."""
         b = self.b
-        if not self._have_minmax:
+        if levels is None and not self._have_minmax:
             self.volume()
         out = torch.empty((b.T, 3, b.h0, b.w0), dtype=torch.float64, device=b.device)
         scratch = torch.empty_like(out)
-        ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [None if t is None else t.data_ptr()
-                                                          for t in self.levels[1:]]))
+        if levels is not None:
+            ptrs = (ctypes.c_void_p * self.nlev)(*[t.data_ptr() for t in levels])
+        else:
+            ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [None if t is None else t.data_ptr()
+                                                              for t in self.levels[1:]]))
         fnum = int(filtering_num) if filtering else 0
         L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, self.nlev, b.T, b.h0, b.w0,
                                   int(bool(sub_pix)), int(filter_window_size), fnum,

@@ -99,6 +99,16 @@ int dm_corr_level12(const dm_tiles *b, void *d_stats, double *d_level1, double *
  * co_map directly (bad_matching.py:62-70).  Needs dm_corr_stats first. */
 int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream);
 
+/* dm_corr_volume with a binary16 volume (uint16_t bit patterns, [T][P][P]): each float32
+ * co_map value rounded to nearest-even half, i.e. np.float16(co_map).  The fp16
+ * correlation volume of BASELINE config C5 (2 B/voxel instead of 4); not bit-exact with
+ * the reference by construction (SURVEY.md 8(a) parity rules: a flip rate is reported).
+ * Needs dm_corr_stats first. */
+int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream);
+
+/* d_out[i] = (double)half(d_in[i]) ** 1.4: _rectification (:158-159) of an fp16 volume. */
+int dm_rectify_f16(const uint16_t *d_in, size_t n, double *d_out, void *stream);
+
 /* d_out[i] = d_in[i] ** 1.4 (pinned float64 pow, dm_pow.h).  Replaces
  * Correlation_map._rectification (:158-159) for the materialised co_map_list[0]. */
 int dm_rectify(const float *d_in, size_t n, double *d_out, void *stream);
@@ -152,7 +162,8 @@ int dm_stitch(const double *d_match, int32_t n0, int32_t n1, int32_t h0, int32_t
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 101 (1.1 adds dm_corr_level12). */
+/* ABI version (major * 100 + minor): 102 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+ * dm_corr_volume_f16 / dm_rectify_f16). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

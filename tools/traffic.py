@@ -1,26 +1,29 @@
 """Per-launch HBM bytes of the level-1 and volume kernels from tools/profile.sh's PMC
 passes: FETCH_SIZE (KiB, x2: gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md HBM
-section) + WRITE_SIZE (KiB).  Writes <dir>/pmc_level1.json and <dir>/pmc_volume.json."""
+section) + WRITE_SIZE (KiB).  Writes <dir>/pmc_level1.json, <dir>/pmc_volume.json and
+<dir>/pmc_volume_f16.json (the binary16 instantiation of the volume kernel)."""
 import csv
 import json
 import os
 import sys
 
-KERNELS = {'level1': ('k_level1_mfq',), 'volume': ('k_volume_cs', 'k_volume_mfq')}
+# key: (kernel name prefixes, f16 instantiation?)
+KERNELS = {'level1': (('k_level1_mfq',), None), 'volume': (('k_volume_cs', 'k_volume_mfq'), False),
+           'volume_f16': (('k_volume_cs',), True)}
 
 
-def per_launch(path, counter, prefix):
+def per_launch(path, counter, prefix, f16=None):
     vals = [float(r['Counter_Value']) for r in csv.DictReader(open(path))
             if r['Counter_Name'] == counter and r['Kernel_Name'].split('<')[0].split('(')[0].strip()
-            .split()[-1] == prefix]
+            .split()[-1] == prefix and (f16 is None or ('_Float16' in r['Kernel_Name']) == f16)]
     return sum(vals) / len(vals) if vals else None
 
 
 def main(root, tile):
-    for key, prefixes in KERNELS.items():
+    for key, (prefixes, f16) in KERNELS.items():
         for prefix in prefixes:
-            f = per_launch(os.path.join(root, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE', prefix)
-            w = per_launch(os.path.join(root, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE', prefix)
+            f = per_launch(os.path.join(root, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE', prefix, f16)
+            w = per_launch(os.path.join(root, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE', prefix, f16)
             if f is not None and w is not None:
                 break
         if f is None or w is None:
