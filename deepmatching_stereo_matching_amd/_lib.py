@@ -22,6 +22,7 @@ DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3,
 DM_TM_CCOEFF, DM_TM_CCOEFF_NORMED = 4, 5
 METHODS = {'cv2.TM_CCOEFF_NORMED': DM_TM_CCOEFF_NORMED, 'cv2.TM_CCOEFF': DM_TM_CCOEFF}
 CAL_MODES = {'elevation': 0, 'elevation2': 1, 'distance': 2}
+DM_GS_FWD4, DM_GS_BWD4, DM_GS_BILAT = 0, 1, 2
 
 
 class DmUnavailable(ImportError):
@@ -60,6 +61,13 @@ SIGNATURES = {
                   _P, _P, _P], ctypes.c_int),
     'dm_sub_pix_cal': ([_P, _P, _I, _I, _I, ctypes.c_double, _P, _P], ctypes.c_int),
     'dm_cal_map': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
+    'dm_gs_schedule': ([_I, _I, _I, _I, _I, _I, _P, _P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    'dm_image_threshold': ([_P, ctypes.c_size_t, ctypes.c_double, ctypes.c_double, _P, _P], ctypes.c_int),
+    'dm_optimize_loop': ([_P, _P, _I, _I, _I, _I, _I, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _I,
+                          _P, _P, _P], ctypes.c_int),
+    'dm_make_weight': ([_P, _I, _I, _I, _I, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P], ctypes.c_int),
+    'dm_opt_loop_bilateral': ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P],
+                              ctypes.c_int),
     'dm_stitch': ([_P, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, _P, _P],
                   ctypes.c_int),
 }

@@ -15,8 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libdmstereo.so')
-SOURCES = [os.path.join(CSRC, 'dm_kernels.hip')]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ('dm_pow.h', 'dm_pow_tables.h', 'dm_mfma.h')
+SOURCES = [os.path.join(CSRC, 'dm_kernels.hip'), os.path.join(CSRC, 'dm_postproc.hip')]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ('dm_pow.h', 'dm_pow_tables.h', 'dm_mfma.h', 'dm_exp.h')
                   if os.path.exists(os.path.join(CSRC, f))] + \
     [os.path.join(REPO, 'include', 'dmstereo.h')]
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

@@ -850,11 +850,18 @@ __global__ void k_stitch(const double *match, int n0, int n1, int h0, int w0, in
 // ------------------------------------------------------------------------------------
 static thread_local char g_err[512];
 
+// shared with dm_postproc.hip (not exported)
+__attribute__((visibility("hidden"))) int dm_vfail(int code, const char *fmt, va_list ap)
+{
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    return code;
+}
+
 static int fail(int code, const char *fmt, ...)
 {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    dm_vfail(code, fmt, ap);
     va_end(ap);
     return code;
 }
@@ -1088,7 +1095,7 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 
 extern "C" {
 
-int dm_abi_version(void) { return 102; }
+int dm_abi_version(void) { return 103; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1287,7 +1294,11 @@ int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *s
                 else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, true, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
                 else k_volume_cs<1, 2, 1, 4, true, 1, true, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);
             } else {
-                if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                const char *vm = getenv("DM_VOLUME_MINW"); // A/B knob: waves per SIMD floor
+                if (NW1 == 4 && vm && vm[0] == '5') k_volume_cs<1, 2, 4, 4, true, 5, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 4 && vm && vm[0] == '6') k_volume_cs<1, 2, 4, 2, true, 6, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 4 && vm && vm[0] == '7') k_volume_cs<1, 2, 4, 4, true, 6, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
+                else if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
                 else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, false, _Float16><<<cgrid, 512, 0, st>>>(gc, s, Bw, QS, out);
                 else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, false, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
                 else k_volume_cs<1, 2, 1, 4, true, 1, false, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);

@@ -5,13 +5,8 @@ import torch
 
 from .. import _lib as L
 from .. import engine
+from .optimize_loop import image_threshold  # noqa: F401  (as the reference imports it, :19)
 
-
-def image_threshold(arr, threshold=[0, 10]):
-    """misc/optimize_loop.py:40-44"""
-    arr = np.where(arr > threshold[1], threshold[1], arr)
-    arr = np.where(arr < threshold[0], threshold[0], arr)
-    return arr
 
 
 def sub_pix_cal(arr, co_map, direction=0, ratio=100.):

@@ -8,6 +8,8 @@
  *   misc/Calc_difference.py  Calc_difference.cal_map (:26-49)
  *   misc/sub_pix_cal.py      sub_pix_cal (:22-53)
  *   misc/image_cut_solver.py ImageCutSolver._execute_matching stitching (:144-179)
+ *   misc/optimize_loop.py    optimize_loop (:15-37), image_threshold (:40-44)
+ *   misc/opt_loop.py         optimize_loop_bilateral_* (:16-58), make_weight (:60-85)
  * The Python mirror of that surface (deepmatching_stereo_matching_amd/misc/) binds
  * these entry points with ctypes; INTEGRATION.md shows the binding.
  *
@@ -159,11 +161,68 @@ int dm_stitch(const double *d_match, int32_t n0, int32_t n1, int32_t h0, int32_t
               int32_t stride0, int32_t stride1, const int32_t *modes, int32_t nmodes,
               double *d_dmap, double *d_score, void *stream);
 
+/* ---- Gauss-Seidel post-processing (dm_postproc.hip) -------------
+ * misc/optimize_loop.py (optimize_loop :15-37, image_threshold :40-44) and misc/opt_loop.py
+ * (optimize_loop_bilateral_horizon :16-35, _vertical :39-58, make_weight :60-85).  Maps are
+ * float64 row-major h x w; `size` = (s0, s1) <= (h, w) bounds the sweeps as in the
+ * reference; excl = `exclusion` (e).  A sweep updates the (s0-2e-1) x (s1-2e-1) cells of
+ * its fixed reference order in place; here it runs as dependency levels (dm_gs_schedule)
+ * and gives the sequential loops' float64 results bit for bit. */
+enum dm_gs_kind {
+    DM_GS_FWD4 = 0,  /* optimize_loop forward sweep, 4-neighbour (optimize_loop.py:18-25)          */
+    DM_GS_BWD4 = 1,  /* optimize_loop backward sweep, with the reference's row alternation (:27-36) */
+    DM_GS_BILAT = 2  /* optimize_loop_bilateral_*, (2e+1)^2 window (opt_loop.py:23-35)              */
+};
+
+/* HOST function (no device work): the dependency-level schedule of one sweep.  n =
+ * max(0, s0-2e-1) * max(0, s1-2e-1) updates; order[n] receives the update sequence indices
+ * grouped by level, level_off[n_levels + 1] (capacity n + 1) the level boundaries.  An
+ * update's level exceeds those of the last writers of every cell it reads and of every
+ * reader of its own cell since that cell's last write, so one level's updates are
+ * independent and the sequential order's values are reproduced exactly. */
+int dm_gs_schedule(int32_t kind, int32_t h, int32_t w, int32_t s0, int32_t s1, int32_t excl,
+                   int32_t *order, int32_t *level_off, int32_t *n_levels);
+
+/* image_threshold (optimize_loop.py:40-44): out = min(max(in, lo), hi) as two np.where
+ * (NaN passes through).  In place allowed. */
+int dm_image_threshold(const double *d_in, size_t n, double lo, double hi, double *d_out,
+                       void *stream);
+
+/* optimize_loop (optimize_loop.py:15-37) on an already thresholded map d_img (in place):
+ * forward sweep then backward sweep of d = (-a x + alpha (L+R+U+D)) / (-a + 4 alpha),
+ * a = coefficient[i, j] (d_coef hc x wc).  Schedules from dm_gs_schedule (DM_GS_FWD4,
+ * DM_GS_BWD4) in device memory.  d_diff: n float64 scratch; *d_error = the backward
+ * sweep's sum of |x - d| in sequence order. */
+int dm_optimize_loop(double *d_img, const double *d_coef, int32_t hc, int32_t wc, int32_t h,
+                     int32_t w, int32_t s0, int32_t s1, int32_t excl, double alpha,
+                     const int32_t *d_fwd_order, const int32_t *d_fwd_off, int32_t fwd_levels,
+                     const int32_t *d_bwd_order, const int32_t *d_bwd_off, int32_t bwd_levels,
+                     double *d_diff, double *d_error, void *stream);
+
+/* make_weight (opt_loop.py:60-85): d_gauss[(2e+1)^2] = exp(-(dy^2+dx^2) / den_space),
+ * d_color[s0-e][s1-e][2e+1][2e+1] = exp(-(c^2) / den_color) with c = guide[i,j] -
+ * guide[i+dy, j+dx] on the filled cells, 0 elsewhere.  den_* = 2.0 * sigma[k]**2 as the
+ * caller's Python evaluates it.  exp is the pinned dm_exp (csrc/dm_exp.h). */
+int dm_make_weight(const double *d_guide, int32_t h, int32_t w, int32_t s0, int32_t s1,
+                   int32_t excl, double den_color, double den_space, double *d_gauss,
+                   double *d_color, void *stream);
+
+/* optimize_loop_bilateral_horizon (vertical = 0) / _vertical (1) (opt_loop.py:16-58):
+ * one sweep of d = (-a b + sum(g cw sub)) / (-a + sum(g cw)) in place on d_img, weights
+ * from dm_make_weight, coefficients coefficient[e, e] and [e, e+-1] / [e+-1, e] of d_coef
+ * (hc x wc), numpy's pairwise sum order.  Schedule: dm_gs_schedule(DM_GS_BILAT).
+ * *d_error = sum of |x - d| in sequence order; d_diff: n float64 scratch. */
+int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_gauss,
+                          const double *d_coef, int32_t hc, int32_t wc, int32_t h, int32_t w,
+                          int32_t s0, int32_t s1, int32_t excl, int32_t vertical,
+                          const int32_t *d_order, const int32_t *d_off, int32_t n_levels,
+                          double *d_diff, double *d_error, void *stream);
+
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 102 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
- * dm_corr_volume_f16 / dm_rectify_f16). */
+/* ABI version (major * 100 + minor): 103 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+ * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

@@ -9,6 +9,8 @@ path.  Heavy loops are in ``dm_oracle.c`` (built by ``oracle/Makefile`` into
   * ``match``        Matching.__call__ with _filter hooks (misc/Matching.py:80-149, 211-222)
   * ``cut_solve``    ImageCutSolver            (misc/image_cut_solver.py:26-184)
   * ``sub_pix_cal``  sub_pix_cal               (misc/sub_pix_cal.py:22-53)
+  * ``optimize_loop``, ``make_weight``, ``opt_loop_bilateral``: the Gauss-Seidel loops of
+    misc/optimize_loop.py:15-44 and misc/opt_loop.py:16-85 (loops in dm_oracle.c)
 
 Parity of this oracle is pinned against ``tests/golden/*.npz`` (generated from the
 reference itself by ``tests/golden/make_golden.py``) in ``tests/test_oracle_golden.py``.
@@ -48,6 +50,14 @@ def lib():
         L.dmo_cal_map.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.dmo_set_pow_mode.argtypes = [ctypes.c_int]
         L.dmo_pow14.argtypes = [ctypes.c_double]
+        I, D = ctypes.c_int, ctypes.c_double
+        L.dmo_optimize_loop.argtypes = [P, P, I, I, I, I, I, I, D]
+        L.dmo_optimize_loop.restype = D
+        L.dmo_make_weight.argtypes = [P, I, I, I, I, D, D, P, P]
+        L.dmo_opt_loop_bilateral.argtypes = [P, P, P, P, I, I, I, I, I, I, I]
+        L.dmo_opt_loop_bilateral.restype = D
+        L.dmo_exp.argtypes = [D]
+        L.dmo_exp.restype = D
         L.dmo_pow14.restype = ctypes.c_double
         _lib = L
     return _lib
@@ -271,3 +281,44 @@ def sub_pix_cal(arr, co_map, direction=0, ratio=100.):
                     dis = d
                 arr[i, j] = dis
     return image_threshold(arr, threshold=[-3, 3])
+
+
+# ---- Gauss-Seidel post-processing -------------------------------
+
+def exp(x):
+    """The pinned float64 exp (csrc/dm_exp.h) the post-processing kernels use."""
+    return lib().dmo_exp(float(x))
+
+
+def optimize_loop(img_dis, coefficient, alpha, exclusion, size):
+    """misc/optimize_loop.py:15-37 -> (thresholded + swept copy, error)."""
+    img = np.ascontiguousarray(image_threshold(np.asarray(img_dis, dtype=np.float64)), dtype=np.float64).copy()
+    coef = np.ascontiguousarray(coefficient, dtype=np.float64)
+    err = lib().dmo_optimize_loop(_p(img), _p(coef), coef.shape[1], img.shape[0], img.shape[1],
+                                  int(size[0]), int(size[1]), int(exclusion), float(alpha))
+    return img, np.float64(err)
+
+
+def make_weight(guide_img, exclusion, size, sigma):
+    """misc/opt_loop.py:60-85 -> (gausian_weight, color_weight_matrix)."""
+    g = np.ascontiguousarray(guide_img, dtype=np.float64)
+    e = int(exclusion)
+    W = 2 * e + 1
+    gauss = np.zeros((W, W))
+    color = np.zeros((size[0] - e, size[1] - e, W, W))
+    lib().dmo_make_weight(_p(g), g.shape[1], int(size[0]), int(size[1]), e,
+                          float(2.0 * sigma[0] ** 2), float(2.0 * sigma[1] ** 2), _p(gauss), _p(color))
+    return gauss, color
+
+
+def opt_loop_bilateral(img_dis, color_weight_matrix, gausian_weight, coefficient, exclusion, size,
+                       vertical=False):
+    """misc/opt_loop.py:16-58 on a float64 copy -> (map, error)."""
+    img = np.array(img_dis, dtype=np.float64, copy=True, order='C')
+    cw = np.ascontiguousarray(color_weight_matrix, dtype=np.float64)
+    gw = np.ascontiguousarray(gausian_weight, dtype=np.float64)
+    coef = np.ascontiguousarray(coefficient, dtype=np.float64)
+    err = lib().dmo_opt_loop_bilateral(_p(img), _p(cw), _p(gw), _p(coef), coef.shape[0], coef.shape[1],
+                                       img.shape[1], int(size[0]), int(size[1]), int(exclusion),
+                                       int(bool(vertical)))
+    return img, np.float64(err)

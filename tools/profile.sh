@@ -19,5 +19,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv 
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
     SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/sq" -o run -- \
     python3 "$REPO/tools/kbench.py" --variants l12 --rounds 2 > "$OUT/sq.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+    SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/sqv16" -o run -- \
+    python3 "$REPO/tools/vbench.py" --f16 --rounds 1 --tiles 32 > "$OUT/sqv16.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/l2v16" -o run -- \
+    python3 "$REPO/tools/vbench.py" --f16 --rounds 1 --tiles 32 > "$OUT/l2v16.log" 2>&1
 python3 "$REPO/tools/traffic.py" "$OUT" 128
 echo done

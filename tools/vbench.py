@@ -1,5 +1,6 @@
 """Volume-kernel A/B timer: dm_corr_volume on the C3 batch (or --tiles of it), variants as
-env settings ("cs", "cs+DM_VOLUME_RB=2", "mfq+DM_VOLUME_CS=0"), interleaved rounds.
+env settings ("cs", "cs+DM_VOLUME_RB=2", "mfq+DM_VOLUME_CS=0"), interleaved rounds; --f16 times the
+binary16 volume (dm_corr_volume_f16).
 
     python tools/vbench.py [--variants cs,mfq+DM_VOLUME_CS=0] [--rounds 3] [--tiles 32]
 """
@@ -15,7 +16,7 @@ from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
 from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
-KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS')
+KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS', 'DM_VOLUME_MINW')
 
 
 def main():
@@ -24,6 +25,7 @@ def main():
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--tile', type=int, default=128)
     ap.add_argument('--tiles', type=int, default=32)
+    ap.add_argument('--f16', action='store_true', help='time dm_corr_volume_f16 (binary16, 2 B/voxel)')
     args = ap.parse_args()
     S, ws = args.tile, 5
     side = 9 * S + ws - 1
@@ -35,7 +37,8 @@ def main():
     lib = L.load()
     batch = engine.TileBatch(ia, ib, org, S, S, ws, L.DM_TM_CCOEFF_NORMED, dev)
     pyr = engine.DevicePyramid(batch, build=False).compute_stats()
-    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float32, device=dev)
+    vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float16 if args.f16 else torch.float32, device=dev)
+    fn = lib.dm_corr_volume_f16 if args.f16 else lib.dm_corr_volume
     res = {v: [] for v in args.variants.split(',')}
     for rnd in range(args.rounds + 1):
         for v in res:
@@ -46,12 +49,12 @@ def main():
                 os.environ[k] = val
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            L.check(lib.dm_corr_volume(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
+            L.check(fn(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
             e1.record()
             torch.cuda.synchronize()
             if rnd:
                 res[v].append(e0.elapsed_time(e1))
-    gb = 4.0 * vol.numel() / 1e9
+    gb = vol.element_size() * vol.numel() / 1e9
     for v, ts in res.items():
         print('%-24s median %8.3f ms  %7.1f GB/s' % (v, np.median(ts), gb / (np.median(ts) * 1e-3)))
 
