@@ -13,7 +13,7 @@
 // sequential order gives it.  One workgroup walks the levels with a barrier between them;
 // the arithmetic per update is the reference's, operation for operation (float64,
 // -ffp-contract=off), so the maps are bit-identical to the sequential loops.  The error
-// sums (`error += abs(...)`) are taken in sequence order by one lane (k_seq_sum).
+// sums (`error += abs(...)`) are taken in sequence order by one dependent chain (k_seq_sum).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -232,21 +232,59 @@ __global__ __launch_bounds__(1024) void k_bilateral(double *img, const double *c
     }
 }
 
-// sum of diff[0..n) in sequence order (the reference's `error += ...`), one lane
-__global__ void k_seq_sum(const double *__restrict__ v, long long n, double *out)
+#include "dm_gs_pf.h"
+
+// sum of diff[0..n) in sequence order (the reference's `error += ...`): one dependent chain
+// of float64 adds that no reordering may shorten.  One wave: chunks of 64 consecutive values
+// are loaded coalesced (one per lane, SEQ_D chunks in flight) and fed to the chain through
+// v_readlane into SGPRs, so the chain runs at the add latency instead of one memory round
+// trip per few elements (the one-lane loop took 36.7 ms per 1M values).
+__device__ __forceinline__ double readlane_d(double v, int k)
 {
-    if (threadIdx.x != 0) return;
-    double acc = 0.0;
-    long long i = 0;
-    for (; i + 8 <= n; i += 8) {
-        double t[8];
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, k);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), k);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+constexpr int SEQ_D = 4;
+
+__global__ __launch_bounds__(64) void k_seq_sum(const double *__restrict__ v, long long n, double *out)
+{
+    const int lane = (int)threadIdx.x;
+    const long long nc = (n + 63) / 64;
+    double x[SEQ_D];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = v[i + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc += t[k];
+    for (int d = 0; d < SEQ_D; ++d) {
+        const long long i = (long long)d * 64 + lane;
+        x[d] = i < n ? v[i] : 0.0;
     }
-    for (; i < n; ++i) acc += v[i];
-    *out = acc;
+    double acc = 0.0; // every lane carries the same chain
+    for (long long c = 0; c < nc; c += SEQ_D) {
+#pragma unroll
+        for (int d = 0; d < SEQ_D; ++d) {
+            const long long cc = c + d;
+            if (cc >= nc) break; // uniform
+            const double cur = x[d];
+            const long long i = (cc + SEQ_D) * 64 + lane;
+            x[d] = i < n ? v[i] : 0.0;
+            const long long m = n - cc * 64;
+            if (m >= 64) {
+#pragma unroll
+                for (int k = 0; k < 64; ++k) acc += readlane_d(cur, k);
+            } else {
+                for (int k = 0; k < (int)m; ++k) acc += readlane_d(cur, k);
+            }
+        }
+    }
+    if (lane == 0) *out = acc;
+}
+
+// (SGPR-fed from wave-uniform s_load blocks instead of readlane measured slower on MI355X:
+// 22 vs 13.8 ms per 1M values -- the chain waits on the scalar loads)
+static void seq_sum(const double *d, long long n, double *out, hipStream_t st)
+{
+    k_seq_sum<<<1, 64, 0, st>>>(d, n, out);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -359,10 +397,14 @@ int dm_optimize_loop(double *d_img, const double *d_coef, int32_t hc, int32_t wc
                      s0, s1, excl);
     if (!d_fwd_order || !d_fwd_off || !d_bwd_order || !d_bwd_off || !d_diff || fwd_levels < 1 || bwd_levels < 1)
         return pfail(DM_ERR_ARG, "missing schedule / diff buffer");
-    k_optimize_loop<<<1, 1024, 0, st>>>(d_img, d_coef, wc, alpha, gf, d_fwd_order, d_fwd_off, fwd_levels, gb,
-                                        d_bwd_order, d_bwd_off, bwd_levels, d_diff);
+    if (gs_pf())
+        k_optimize_loop_pf<<<1, 1024, 0, st>>>(d_img, d_coef, wc, alpha, gf, d_fwd_order, d_fwd_off, fwd_levels, gb,
+                                               d_bwd_order, d_bwd_off, bwd_levels, d_diff);
+    else
+        k_optimize_loop<<<1, 1024, 0, st>>>(d_img, d_coef, wc, alpha, gf, d_fwd_order, d_fwd_off, fwd_levels, gb,
+                                            d_bwd_order, d_bwd_off, bwd_levels, d_diff);
     PHIP_TRY(hipGetLastError());
-    k_seq_sum<<<1, 64, 0, st>>>(d_diff, n, d_error);
+    seq_sum(d_diff, n, d_error, st);
     PHIP_TRY(hipGetLastError());
     return DM_OK;
 }
@@ -404,10 +446,24 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
         return pfail(DM_ERR_SHAPE, "index %d is out of bounds for the %dx%d coefficient", excl + 1, hc, wc);
     if (!d_color || !d_gauss || !d_order || !d_off || !d_diff || n_levels < 1)
         return pfail(DM_ERR_ARG, "missing weights / schedule / diff buffer");
-    k_bilateral<<<1, 1024, 0, st>>>(d_img, d_color, d_gauss, d_coef, hc, wc, vertical ? 1 : 0, g, d_order, d_off,
-                                    n_levels, d_diff);
+    const int vt = vertical ? 1 : 0;
+#define DM_BILAT_PF(E_, LPU_, R_, NT_)                                                                            \
+    k_bilateral_pf<E_, LPU_, R_, NT_><<<1, NT_, 0, st>>>(d_img, d_color, d_gauss, d_coef, hc, wc, vt, g, d_order, d_off,  \
+                                                 n_levels, d_diff)
+    const bool pf = gs_pf();
+    // lanes per update, prefetched rounds, workgroup size: ~n/(e+1) updates per level of an
+    // n = 1024 map prefetched without spilling (128 VGPRs per lane at 1024 lanes, 256 at 512)
+    if (pf && excl == 1) DM_BILAT_PF(1, 4, 1, 1024);
+    else if (pf && excl == 2) DM_BILAT_PF(2, 4, 1, 1024);
+    else if (pf && excl == 3) DM_BILAT_PF(3, 4, 2, 512);
+    else if (pf && excl == 4) DM_BILAT_PF(4, 8, 2, 512);
+    else if (pf && excl == 5) DM_BILAT_PF(5, 8, 1, 512);
+    else
+        k_bilateral<<<1, 1024, 0, st>>>(d_img, d_color, d_gauss, d_coef, hc, wc, vt, g, d_order, d_off, n_levels,
+                                        d_diff);
+#undef DM_BILAT_PF
     PHIP_TRY(hipGetLastError());
-    k_seq_sum<<<1, 64, 0, st>>>(d_diff, n, d_error);
+    seq_sum(d_diff, n, d_error, st);
     PHIP_TRY(hipGetLastError());
     return DM_OK;
 }

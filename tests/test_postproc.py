@@ -267,3 +267,55 @@ def test_gpu_image_threshold_and_errors():
         optimize_loop_bilateral_horizon(np.ones((8, 8)), c, g, np.ones((2, 2)), 0.0, 1, (8, 8))
     out, err = optimize_loop(np.full((5, 9), 20.0), np.ones((5, 9)), 0.008, 2, (5, 9))   # no update
     assert same(out, np.full((5, 9), 10.0)) and err == 0.0
+
+
+# ---------------------------------------------------------------------------------------
+# GPU: the pipelined level walks (k_optimize_loop_pf, k_bilateral_pf; DM_GS_PF=0 selects
+# the one-lane-per-update kernels) -- every exclusion they instantiate, levels wider than
+# one round of the workgroup, and the fallback (e = 6)
+# ---------------------------------------------------------------------------------------
+def _bilateral_case(n, e, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:n, 0:n]
+    guide = 5 + 4 * np.sin(x / 13.0) * np.cos(y / 7.0) + rng.normal(0, 0.7, (n, n))
+    coef = rng.uniform(0.2, 1.5, (n, n))
+    return guide, coef
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('n,e', [(40, 1), (61, 2), (300, 1), (150, 3), (90, 4), (700, 4), (70, 5), (50, 6),
+                                 (800, 2)])
+def test_gpu_bilateral_pipelined(n, e, monkeypatch):
+    import torch
+    from deepmatching_stereo_matching_amd.misc import opt_loop as M
+    guide, coef = _bilateral_case(n, e, n + e)
+    og, oc = O.make_weight(guide, e, (n, n), [5, 5])
+    dev = torch.device('cuda', 0)
+    tc, tg = torch.from_numpy(oc).to(dev), torch.from_numpy(og).to(dev)
+    tcoef = torch.from_numpy(coef).to(dev)
+    for vert in (False, True):
+        ref, rerr = O.opt_loop_bilateral(guide, oc, og, coef, e, (n, n), vert)
+        fn = M.optimize_loop_bilateral_vertical if vert else M.optimize_loop_bilateral_horizon
+        outs = []
+        for pf in ('1', '0'):
+            monkeypatch.setenv('DM_GS_PF', pf)
+            timg = torch.from_numpy(guide).to(dev)
+            _, err = fn(timg, tc, tg, tcoef, 0.008, e, (n, n))
+            outs.append((timg.cpu().numpy(), float(err)))
+        for out, err in outs:
+            assert same(out, ref) and err == rerr, (vert, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('h,w,e', [(1100, 1100, 1), (33, 1030, 0), (257, 64, 2)])
+def test_gpu_optimize_loop_pipelined(h, w, e, monkeypatch):
+    from deepmatching_stereo_matching_amd.misc.optimize_loop import optimize_loop
+    rng = np.random.default_rng(h * w + e)
+    img = rng.uniform(-2, 12, (h, w))
+    coef = rng.uniform(0, 2, (h, w))
+    size = (h - 1, w - 1) if e == 0 else (h, w)    # e = 0: the backward sweep reads row s0 - e
+    ref, rerr = O.optimize_loop(img, coef, 0.008, e, size)
+    for pf in ('1', '0'):
+        monkeypatch.setenv('DM_GS_PF', pf)
+        out, err = optimize_loop(img, coef, 0.008, e, size)
+        assert same(out, ref) and same_err(err, rerr), pf
