@@ -12,11 +12,27 @@ KERNELS = {'level1': (('k_level1_mfq',), None), 'volume': (('k_volume_cs', 'k_vo
            'volume_f16': (('k_volume_cs',), True)}
 
 
+def _is(name, prefix):
+    """demangled ('void k_volume_cs<...>(...)') or mangled ('_Z11k_volume_csI...') name"""
+    if name.startswith('_Z'):
+        return ('%d%sI' % (len(prefix), prefix)) in name[:len(prefix) + 8]
+    return name.split('<')[0].split('(')[0].strip().split()[-1] == prefix
+
+
+def _f16(name):
+    return '_Float16' in name or 'DF16_' in name
+
+
 def per_launch(path, counter, prefix, f16=None):
+    """mean over the full-size launches (>= half the largest: bench.py's one-tile flip-rate
+    batches use the same kernel on far fewer tiles)"""
     vals = [float(r['Counter_Value']) for r in csv.DictReader(open(path))
-            if r['Counter_Name'] == counter and r['Kernel_Name'].split('<')[0].split('(')[0].strip()
-            .split()[-1] == prefix and (f16 is None or ('_Float16' in r['Kernel_Name']) == f16)]
-    return sum(vals) / len(vals) if vals else None
+            if r['Counter_Name'] == counter and _is(r['Kernel_Name'], prefix)
+            and (f16 is None or _f16(r['Kernel_Name']) == f16)]
+    if not vals:
+        return None
+    big = [v for v in vals if v >= 0.5 * max(vals)]
+    return sum(big) / len(big)
 
 
 def main(root, tile):
