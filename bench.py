@@ -7,11 +7,17 @@ cal_map and stitching -- i.e. ImageCutSolver(img1, img2, image_size=[128,128],
 stride=[128,128], window_size=5)() on the GPU.  One step = one pair; inputs are
 resident in HBM before the timed region.  V = 64 tiles x 128^4 = 17.18 G voxels/pair.
 
-Multi-GPU (torchrun, one process per GPU): every rank solves its own pairs (pairs are
-independent: weak scaling, no collective on the data path); timing is barrier +
-synchronize bracketed, max over ranks.
+Multi-GPU (one process per GPU, torch.distributed; `--gpus N` without WORLD_SIZE in the
+environment launches N ranks itself through torch.distributed.run before touching the GPU):
+  c2/c3  every rank solves its own pair per step (pairs are independent: weak scaling, no
+         collective on the data path);
+  c4     BASELINE configs[3]: one step is a batch of 64 independent pairs, rank r solves
+         pairs r::N (strong scaling over the fixed batch; no collective);
+  c5     one 4096^2 pair per step, its 256 tiles sharded over the ranks, results
+         all-gathered (RCCL over xGMI) and stitched (strong scaling).
+Timing is barrier + synchronize bracketed, max over ranks.
 
-Also reported: the roofline of the dominant kernel (dm_corr_level1), timed with HIP
+Also reported: the roofline of the dominant kernel (dm_corr_level12), timed with HIP
 events on the launch stream inside the timed steps, the HBM roofline of the level-0
 volume kernel (dm_corr_volume, 4 B/voxel written, and its fp16 variant, 2 B/voxel) on the
 same batch, the fp16 volume's argmax flip rate, and the CPU oracle's rate on a bounded
@@ -38,7 +44,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 WS = 5
 S = 128
 GRID = 8
-CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
+CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c4': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
+C4_PAIRS = 64                  # BASELINE configs[3]: a batch of 64 independent 1024^2 pairs
 VOLUME_BUDGET = 64e9           # bytes of level-0 volume materialised for its roofline
 
 
@@ -49,7 +56,8 @@ def parse():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
                     help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
-                         'c5 (4096^2, S=256)')
+                         'c4 (64 pairs of c3 per step, sharded over the ranks), c5 (4096^2, S=256)')
+    ap.add_argument('--pairs', type=int, default=C4_PAIRS, help='c4: pairs per step (whole job)')
     ap.add_argument('--tile', type=int, default=None)
     ap.add_argument('--grid', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -196,11 +204,96 @@ def load_traffic(tile, kernel='level1'):
     return load_pmc(tile, kernel).get('hbm_bytes_per_launch')
 
 
+def level_roofline(solver, tile, l1_ms):
+    """Roofline of the dominant kernel, dm_corr_level12 (k_level1_mfq): levels 0 -> 1 -> 2 in
+    one pass, level 0 and level 1 never leave the chip.
+
+    It is compute-bound: its physical HBM traffic (PMC, ~1.24 GB per C3 launch) is ~1.5 % of
+    what the bandwidth would allow in its run time.  The bound is the vector ALU (float32
+    normalisation, float64 pow14 of every pooled child value), so `achieved` / `peak` are
+    VALU-busy SIMD-cycles per second against 1024 SIMDs x the clock the kernel ran at, both
+    from a committed rocprofv3 --pmc pass (profiles/pmc_level1.json, tools/pmc_valu.sh):
+    SQ_ACTIVE_INST_VALU (quad-cycles) x 4 per launch over the live HIP-event time, and the
+    effective clock GRBM_GUI_ACTIVE / 8 XCDs / profiled kernel time.  The 4 B/voxel figure of
+    SURVEY.md 8(d) (the level-0 volume this kernel does not write) is kept as
+    `hbm_equivalent`."""
+    vox_launch = solver.batch.T * float(tile) ** 4   # this rank's tiles per launch
+    gbs = 4.0 * vox_launch / (l1_ms * 1e-3) / 1e9
+    mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
+    kname = ('dm_corr_level1 (k_level1_mfq)' if mode == 0
+             else 'dm_corr_level12 (k_level1_mfq, level 2 fused)')
+    pmc = load_pmc(tile) if solver.batch.T == 64 else {}
+    roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3)}
+    busy, clk = pmc.get('valu_active_cycles_per_launch'), pmc.get('clock_ghz')
+    if busy and clk:
+        achieved = busy / (l1_ms * 1e-3) / 1e9          # G SIMD-cycles/s with the VALU busy
+        peak = 1024 * clk
+        roof.update({'achieved': round(achieved, 1), 'peak': round(peak, 1),
+                     'unit': 'G VALU-busy SIMD-cycles/s', 'frac': round(achieved / peak, 4),
+                     'valu_busy_source': 'SQ_ACTIVE_INST_VALU x4 per launch (PMC) / live time; '
+                                         'peak 1024 SIMDs x %.3f GHz (GRBM_GUI_ACTIVE/8/t)' % clk})
+    else:
+        roof.update({'achieved': None, 'peak': None, 'unit': 'G VALU-busy SIMD-cycles/s',
+                     'frac': None, 'valu_busy_source': 'no PMC pass for this batch shape'})
+    if pmc.get('valu_insts_per_launch'):
+        # issue-limited estimate: a wave64 VALU instruction occupies a 32-lane SIMD >= 2 cycles
+        roof['valu_insts_per_launch'] = pmc['valu_insts_per_launch']
+    roof['traffic'] = load_traffic(tile) if pmc else None
+    roof['hbm_equivalent'] = {'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                              'frac': round(gbs / HBM_PEAK_GBS, 4),
+                              'algorithmic': '4 B/voxel x %d level-0 voxels per launch (never '
+                                             'written: the volume a materialising kernel would '
+                                             'store)' % int(vox_launch)}
+    return roof
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed environment: run
+    N ranks (one per GPU) under torch.distributed.run as a CHILD process and return its exit
+    status.  This process has not initialised the GPU (torch.cuda.device_count() does not on
+    this image), and it never exec()s."""
+    import socket
+    import subprocess
+    n = torch.cuda.device_count()
+    if n < args.gpus:
+        raise SystemExit('bench.py --gpus %d: only %d GPU(s) visible' % (args.gpus, n))
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def make_pairs(args, tile, grid, rank, world):
+    """Synthetic input pairs of this rank (SURVEY.md 8(d) generator; seed 1000 + pair index)
+    -> (list of (img1, img2) host arrays, pair indices, pairs per step for the whole job)."""
+    # ImageCutSolver's floor rule (image_cut_solver.py:62): floor((side - (tile+ws-1)) / tile)
+    # tiles per axis, so a grid x grid cut needs side = (grid+1)*tile + ws-1 (1156 for C3)
+    side = (grid + 1) * tile + WS - 1
+    if args.config == 'c4':
+        from deepmatching_stereo_matching_amd import shard
+        idx = shard.rank_units(args.pairs, rank, world)
+        job_pairs = args.pairs
+    elif args.config == 'c5' and world > 1:
+        idx, job_pairs = [0], 1       # one pair, tiles split over the ranks
+    else:
+        idx, job_pairs = [rank], world
+    pairs = [stereo_pair(side, side, seed=1000 + i, dx=2, max_disp=tile // 4, sinusoidal=True)
+             for i in idx]
+    return pairs, idx, job_pairs
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit('bench.py --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -208,30 +301,42 @@ def main():
         tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local if dist else 0)
     torch.cuda.set_device(dev)
+    joined = world
+    if dist:   # ranks that actually joined the job
+        j = torch.ones(1, dtype=torch.int64, device=dev)
+        tdist.all_reduce(j)
+        joined = int(j.item())
+        if joined != args.gpus:
+            raise SystemExit('bench.py --gpus %d: %d ranks joined' % (args.gpus, joined))
 
     tile, grid = CONFIGS[args.config]
     tile, grid = args.tile or tile, args.grid or grid
-    # ImageCutSolver's floor rule (image_cut_solver.py:62): floor((side - (tile+ws-1)) / tile)
-    # tiles per axis, so a grid x grid cut needs side = (grid+1)*tile + ws-1 (1156 for C3)
-    side = (grid + 1) * tile + WS - 1
     # c5 (BASELINE configs[4]): ONE pair per step, its tiles sharded over the ranks (strong
-    # scaling, results all-gathered); c2/c3: one pair per rank per step (weak scaling)
+    # scaling, results all-gathered); c4: a fixed batch of pairs split over the ranks
+    # (strong scaling); c2/c3: one pair per rank per step (weak scaling)
     split = args.config == 'c5' and world > 1
-    a, b = stereo_pair(side, side, seed=1000 + (0 if split else rank), dx=2, max_disp=tile // 4,
-                       sinusoidal=True)
-    img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
-    solver = PairSolver(img1, img2, tile, grid, split=split)
-    voxels = solver.T * float(tile) ** 4      # per pair
+    host_pairs, pair_idx, job_pairs = make_pairs(args, tile, grid, rank, world)
+    solvers = []
+    for a, b in host_pairs:
+        img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+        solvers.append(PairSolver(img1, img2, tile, grid, split=split))
+    del host_pairs
+    solver = solvers[0] if solvers else None
+    voxels = grid * grid * float(tile) ** 4      # per pair
+
+    def step(timed=False):
+        for s in solvers:
+            s.step(timed=timed)
 
     for _ in range(args.warmup):
-        solver.step()
+        step()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        solver.step(timed=True)
+        step(timed=True)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -243,39 +348,34 @@ def main():
         elapsed = float(t.item())
 
     ms_step = elapsed / args.steps * 1e3
-    pairs = 1 if split else world                 # pairs solved per step by the whole job
-    value = pairs * args.steps * voxels / elapsed / 1e9
-    l1_ms = solver.level1_ms()
+    value = job_pairs * args.steps * voxels / elapsed / 1e9
+    l1_ms = solver.level1_ms() if solver else None
+    if rank == 0 and solver is None:
+        raise SystemExit('rank 0 has no pairs (--pairs < --gpus)')
     if rank == 0:
-        # dominant kernel: the fused level-0 -> level-1 (-> level-2) kernel.  Algorithmic bytes per
-        # 4 B per level-0 voxel (the volume a materialising L0 kernel
-        # writes); this kernel keeps level 0 on chip, so "achieved" is the HBM-equivalent
-        # rate and "traffic" (PMC) the bytes it really moves.
-        vox_launch = solver.batch.T * float(tile) ** 4   # this rank's tiles per launch
-        gbs = 4.0 * vox_launch / (l1_ms * 1e-3) / 1e9
-        mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
-        kname = 'dm_corr_level1 (k_level1_mfq)' if mode == 0 else 'dm_corr_level12 (k_level1_mfq, level 2 fused)'
-        roof = {'kernel': kname, 'bound': 'hbm', 'ms': round(l1_ms, 3),
-                'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': load_traffic(tile),
-                'algorithmic': '4 B/voxel x %d voxels per launch (level 0 never leaves the chip)'
-                               % int(vox_launch)}
-        # what actually bounds it: VALU issue (f64 pow + f32 normalisation), from the PMC
-        # VALU instruction count: wave64 VALU op = 4 cycles on a SIMD, 1024 SIMDs, 2.4 GHz
-        valu = load_pmc(tile).get('valu_insts_per_launch') if world == 1 else None
-        if valu:
-            roof['valu_issue_frac'] = round(valu * 4.0 / (1024 * l1_ms * 1e-3 * 2.4e9), 3)
+        roof = level_roofline(solver, tile, l1_ms)
+        if args.config == 'c4':
+            workload = ('C4: batch of %d independent %dx%d pairs per step (%dx%d tiles of S=%d each), '
+                        'ws=%d, full pyramid + sub-pixel + cal_map + stitch'
+                        % (job_pairs, grid * tile, grid * tile, grid, grid, tile, WS))
+            per_gpu, par = job_pairs / float(world), 'pairs of the batch sharded %d-way' % world
+        else:
+            workload = ('%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
+                        '+ sub-pixel + cal_map + stitch'
+                        % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS))
+            per_gpu = (1.0 / world) if split else 1
+            par = ('tiles of one pair sharded %d-way' if split else 'pairs sharded %d-way') % world
         rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
-               'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': world, 'steps': args.steps,
-               'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
-               'scaling': 'strong' if split else 'weak', 'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
+               'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': joined, 'steps': args.steps,
+               'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),
+               'ms_per_pair': round(ms_step / job_pairs * world, 3),
+               'higher_is_better': True,
+               'scaling': 'strong' if (split or args.config == 'c4') else 'weak',
+               'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
                'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
-               'config': {'workload': '%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
-                                      '+ sub-pixel + cal_map + stitch'
-                                      % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS),
-                          'tile': tile, 'tiles_per_pair': grid * grid, 'window_size': WS,
-                          'pairs_per_gpu_per_step': (1.0 / world) if split else 1,
-                          'parallelism': ('tiles of one pair sharded %d-way' if split else 'pairs sharded %d-way') % world},
+               'config': {'workload': workload, 'tile': tile, 'tiles_per_pair': grid * grid,
+                          'window_size': WS, 'pairs_per_step': job_pairs,
+                          'pairs_per_gpu_per_step': per_gpu, 'parallelism': par},
                'roofline': roof}
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)

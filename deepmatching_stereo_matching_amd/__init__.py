@@ -25,7 +25,7 @@ def alias_misc():
     pkg = importlib.import_module(__name__ + '.misc')
     sys.modules.setdefault('misc', pkg)
     for sub in ('Correlation_map', 'Matching', 'Calc_difference', 'Feature_value', 'image_cut_solver',
-                'loader', 'raw_read', 'sub_pix_cal'):
+                'loader', 'raw_read', 'sub_pix_cal', 'optimize_loop', 'opt_loop'):
         mod = importlib.import_module('%s.misc.%s' % (__name__, sub))
         sys.modules.setdefault('misc.' + sub, mod)
     return pkg

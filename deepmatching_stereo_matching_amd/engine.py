@@ -8,6 +8,7 @@ device pointers on the current torch stream.  Reference call stack it replaces:
 (misc/Calc_difference.py:26-49), per tile of ``ImageCutSolver`` (misc/image_cut_solver.py).
 """
 
+import contextlib
 import ctypes
 import os
 
@@ -313,26 +314,35 @@ def tile_bytes(h0, w0):
     return total
 
 
+def _on(stream):
+    """Run a block with ``stream`` as torch's current stream, so that the library calls
+    (launched on the current stream), the copies and the caching allocator's frees are all
+    ordered on it."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
 def solve_tiles(img1, img2, origins, h0, w0, ws, method, sub_pix=True, filtering=False,
                 filter_window_size=3, filtering_num=3, filtering_mode='median',
                 device=None, mem_budget=None, stream=None):
     """Correlation_map + Matching for every tile; float64 [T][3][h0][w0] device tensor.
-    Tiles are processed in chunks that fit ``mem_budget`` bytes of HBM."""
+    Tiles are processed in chunks that fit ``mem_budget`` bytes of HBM.  Everything,
+    allocations included, is ordered on ``stream`` (default: the current stream)."""
     device = device or default_device()
-    img1 = to_device_u8(img1, device)
-    img2 = to_device_u8(img2, device)
-    origins = np.asarray(origins, dtype=np.int64).reshape(-1, 2)
-    if mem_budget is None:
-        mem_budget = int(os.environ.get('DM_MEM_BUDGET', 64 << 30))
-    per = tile_bytes(h0, w0)
-    chunk = max(1, min(len(origins), mem_budget // max(per, 1)))
-    out = torch.empty((len(origins), 3, h0, w0), dtype=torch.float64, device=device)
-    for s in range(0, len(origins), chunk):
-        b = TileBatch(img1, img2, origins[s:s + chunk], h0, w0, ws, method, device)
-        pyr = DevicePyramid(b, stream=stream)
-        out[s:s + len(b.origins_host)] = pyr.match(sub_pix, filtering, filter_window_size,
-                                                   filtering_num, filtering_mode)
-        del pyr, b
+    with _on(stream):
+        img1 = to_device_u8(img1, device)
+        img2 = to_device_u8(img2, device)
+        origins = np.asarray(origins, dtype=np.int64).reshape(-1, 2)
+        if mem_budget is None:
+            mem_budget = int(os.environ.get('DM_MEM_BUDGET', 64 << 30))
+        per = tile_bytes(h0, w0)
+        chunk = max(1, min(len(origins), mem_budget // max(per, 1)))
+        out = torch.empty((len(origins), 3, h0, w0), dtype=torch.float64, device=device)
+        for s in range(0, len(origins), chunk):
+            b = TileBatch(img1, img2, origins[s:s + chunk], h0, w0, ws, method, device)
+            pyr = DevicePyramid(b)
+            out[s:s + len(b.origins_host)] = pyr.match(sub_pix, filtering, filter_window_size,
+                                                       filtering_num, filtering_mode)
+            del pyr, b
     return out
 
 
@@ -340,10 +350,12 @@ def stitch(match, n, h0, w0, stride, modes, stream=None):
     """ImageCutSolver._execute_matching stitching on the device -> (d_map, out_map)."""
     mode_ids = [L.CAL_MODES[m] for m in modes]
     Hout, Wout = stride[0] * (n[0] - 1) + h0, stride[1] * (n[1] - 1) + w0
-    dmap = torch.empty((len(modes), Hout, Wout), dtype=torch.float64, device=match.device)
-    score = torch.empty((Hout, Wout), dtype=torch.float64, device=match.device)
-    arr = (ctypes.c_int32 * max(1, len(mode_ids)))(*mode_ids)
-    L.check(L.load().dm_stitch(L.ptr(match.contiguous()), n[0], n[1], h0, w0, stride[0],
-                               stride[1], arr, len(mode_ids), L.ptr(dmap), L.ptr(score),
-                               L.stream_handle(stream)), 'dm_stitch')
+    with _on(stream):
+        m = match.contiguous()
+        dmap = torch.empty((len(modes), Hout, Wout), dtype=torch.float64, device=match.device)
+        score = torch.empty((Hout, Wout), dtype=torch.float64, device=match.device)
+        arr = (ctypes.c_int32 * max(1, len(mode_ids)))(*mode_ids)
+        L.check(L.load().dm_stitch(L.ptr(m), n[0], n[1], h0, w0, stride[0], stride[1], arr,
+                                   len(mode_ids), L.ptr(dmap), L.ptr(score), L.stream_handle()),
+                'dm_stitch')
     return dmap, score

@@ -5,7 +5,7 @@ import sys
 import numpy as np
 import torch
 
-from .. import engine
+from deepmatching_stereo_matching_amd import engine
 
 
 class Calc_difference():

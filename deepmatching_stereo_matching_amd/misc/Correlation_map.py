@@ -14,13 +14,10 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .. import _lib as L
-from .. import engine
+from deepmatching_stereo_matching_amd import _lib as L
+from deepmatching_stereo_matching_amd import engine
 
-try:
-    from .Feature_value import Feature_value
-except ImportError:  # pragma: no cover
-    from Feature_value import Feature_value
+from deepmatching_stereo_matching_amd.misc.Feature_value import Feature_value
 
 
 class LevelList(Sequence):
@@ -108,7 +105,6 @@ class Correlation_map():
                              '({1},{1})'.format(ws - 1, ws))
         win = np.lib.stride_tricks.sliding_window_view(img, (ws, ws))[:h0, :w0]
         self.atomic_patch = np.ascontiguousarray(win).astype(np.uint8)
-        self._device_pyramid(build=False)
 
     def _create_simple_initial_co_map(self):
         '''

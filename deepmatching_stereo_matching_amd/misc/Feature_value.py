@@ -9,8 +9,8 @@ import sys
 import numpy as np
 import torch
 
-from .. import _lib as L
-from .. import engine
+from deepmatching_stereo_matching_amd import _lib as L
+from deepmatching_stereo_matching_amd import engine
 
 
 class Feature_value():

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .. import engine
+from deepmatching_stereo_matching_amd import engine
 
 
 class Matching():

@@ -11,11 +11,8 @@ import numpy as np
 import torch
 from PIL import Image
 
-from .. import _lib as L
-from .. import engine
-from .Calc_difference import Calc_difference
-from .Correlation_map import Correlation_map
-from .Matching import Matching
+from deepmatching_stereo_matching_amd import _lib as L
+from deepmatching_stereo_matching_amd import engine
 
 
 class ImageCutSolver():
@@ -46,7 +43,7 @@ class ImageCutSolver():
         self.trimed_size = [image_size[i] + 2 * self.exclusive_pix for i in range(2)]
         self.feature_name = feature_name
         if feature_name not in L.METHODS:
-            from .Feature_value import Feature_value
+            from deepmatching_stereo_matching_amd.misc.Feature_value import Feature_value
             Feature_value(feature_name)  # prints + exits like the reference
 
         if padding:
@@ -90,32 +87,48 @@ class ImageCutSolver():
 
     def _solver(self, solve_image, solve_template):
         """
-        小画像に対しdeepmatchingを実施する (one tile, through the mirror classes)
+        小画像に対しdeepmatchingを実施する: one (S+2e)^2 crop pair -> (d_maps, score map),
+        as the reference's _solver (:115-142) returns them; solved by the same batched device
+        path as _execute_matching (a batch of one tile).
         """
-        co_cls = Correlation_map(solve_image, solve_template, window_size=self.window_size, feature_name=self.feature_name)
-        co_cls()
-        if self.log_flg:
-            print('complete to create multi-level correlation pyramid')
-            print('pyramid level: {}, N={}'.format(co_cls.iteration, co_cls.N_map))
-            self.log_flg = False
-        cls = Matching(co_cls, sub_pix=self.sub_pix, filtering=self.filtering, filter_window_size=self.filtering_window_size, filtering_num=self.filtering_num, filtering_mode=self.filtering_mode)
-        out = cls()
-        return np.array([Calc_difference.cal_map(out, mode=mode_here) for mode_here in self.degree_map_mode]), out[2, :, :]
+        h0 = np.shape(solve_image)[0] - 2 * self.exclusive_pix
+        w0 = np.shape(solve_image)[1] - 2 * self.exclusive_pix
+        self._log_pyramid(h0, w0)
+        match = engine.solve_tiles(solve_image, solve_template, [[0, 0]], h0, w0, self.window_size,
+                                   L.METHODS[self.feature_name], self.sub_pix, self.filtering,
+                                   self.filtering_window_size, self.filtering_num,
+                                   self.filtering_mode)[0]
+        d = np.array([engine.cal_map(match, m).cpu().numpy() for m in self.degree_map_mode])
+        return d, match[2].cpu().numpy()
 
-    def _execute_matching_device(self):
-        """All tiles in batches on the GPU -> (d_map, out_map) device tensors."""
-        n, origins = engine.cut_grid(self.img1.shape, self.image_size, self.stride,
-                                     self.window_size)
-        h0, w0 = self.image_size
+    def _log_pyramid(self, h0, w0):
         if self.log_flg:
             nlev, N = engine.pyramid_plan(h0, w0)
             print('complete to create multi-level correlation pyramid')
             print('pyramid level: {}, N={}'.format(nlev, N))
             self.log_flg = False
-        match = engine.solve_tiles(self.img1, self.img2, origins, h0, w0, self.window_size,
-                                   L.METHODS[self.feature_name], self.sub_pix, self.filtering,
-                                   self.filtering_window_size, self.filtering_num,
-                                   self.filtering_mode)
+
+    def _execute_matching_device(self):
+        """All tiles in batches on the GPU -> (d_map, out_map) device tensors.  The tile grid
+        is self.len, counted on the image shape BEFORE _padding (:46,58-62).  With a
+        torch.distributed process group initialised, the tiles are sharded over its ranks
+        (shard.solve_tiles_sharded: rank r solves tiles r::N, results all-gathered) and every
+        rank stitches the whole map."""
+        from deepmatching_stereo_matching_amd import shard
+        n = list(self.len)
+        if n[0] < 1 or n[1] < 1:
+            raise IndexError('list index out of range')   # img_index[-1] of an empty cut (:150)
+        origins = np.array([(self.stride[0] * i, self.stride[1] * j)
+                            for j in range(n[1]) for i in range(n[0])], dtype=np.int64)
+        h0, w0 = self.image_size
+        self._log_pyramid(h0, w0)
+        args = (self.img1, self.img2, origins, h0, w0, self.window_size,
+                L.METHODS[self.feature_name], self.sub_pix, self.filtering,
+                self.filtering_window_size, self.filtering_num, self.filtering_mode)
+        if shard.world()[1] > 1:
+            match = shard.solve_tiles_sharded(*args)
+        else:
+            match = engine.solve_tiles(*args)
         return engine.stitch(match, n, h0, w0, self.stride, self.degree_map_mode)
 
     def _execute_matching(self):

@@ -10,8 +10,8 @@ Documented deviation: the reference's ``assert type(path) == 'str'`` is always f
 
 import numpy as np
 
-from ..imageio import imread_bgr as _imread_bgr
-from ..imageio import imread_gray as _imread_gray
+from deepmatching_stereo_matching_amd.imageio import imread_bgr as _imread_bgr
+from deepmatching_stereo_matching_amd.imageio import imread_gray as _imread_gray
 
 
 class Loader():

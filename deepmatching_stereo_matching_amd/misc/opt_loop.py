@@ -12,7 +12,7 @@ tensors out, swept in place with no copies.
 import numpy as np
 import torch
 
-from .. import postproc
+from deepmatching_stereo_matching_amd import postproc
 
 
 def _sweep(img_dis, color_weight_matrix, gausian_weight, coefficient, exclusion, size, vertical):

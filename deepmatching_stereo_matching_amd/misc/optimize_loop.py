@@ -9,7 +9,7 @@ numpy in -> numpy out; a float64 GPU tensor in -> tensor out (error stays a devi
 import numpy as np
 import torch
 
-from .. import postproc
+from deepmatching_stereo_matching_amd import postproc
 
 
 def image_threshold(arr, threshold=[0, 10]):

@@ -3,9 +3,9 @@
 import numpy as np
 import torch
 
-from .. import _lib as L
-from .. import engine
-from .optimize_loop import image_threshold  # noqa: F401  (as the reference imports it, :19)
+from deepmatching_stereo_matching_amd import _lib as L
+from deepmatching_stereo_matching_amd import engine
+from deepmatching_stereo_matching_amd.misc.optimize_loop import image_threshold  # noqa: F401  (as the reference imports it, :19)
 
 
 

@@ -28,21 +28,26 @@ def rank_units(n, rank, size):
 
 
 def _gather_units(local, n, rank, size, shape, dtype):
-    """All-gather per-rank unit results ([k_r][*shape]) back into unit order [n][*shape]."""
+    """All-gather per-rank unit results ([k_r][*shape]) back into unit order [n][*shape].
+    With the nccl (RCCL) backend the gather runs device to device over xGMI; a gloo group
+    (CPU tests, or ranks sharing one GPU) gathers host copies and the result goes back to
+    ``local``'s device."""
     per = (n + size - 1) // size
-    buf = torch.zeros((per,) + tuple(shape), dtype=dtype, device=local.device)
+    host = size > 1 and local.is_cuda and dist.get_backend() == 'gloo'
+    dev = local.device
+    buf = torch.zeros((per,) + tuple(shape), dtype=dtype, device='cpu' if host else dev)
     if len(local):
         buf[:len(local)] = local
     if size == 1:
         return buf[:n]
     parts = [torch.empty_like(buf) for _ in range(size)]
     dist.all_gather(parts, buf)
-    out = torch.empty((n,) + tuple(shape), dtype=dtype, device=local.device)
+    out = torch.empty((n,) + tuple(shape), dtype=dtype, device=buf.device)
     for r in range(size):
         idx = rank_units(n, r, size)
         if idx:
             out[idx] = parts[r][:len(idx)]
-    return out
+    return out.to(dev) if host else out
 
 
 def solve_tiles_sharded(img1, img2, origins, h0, w0, ws, method, sub_pix=True, filtering=False,

@@ -8,6 +8,8 @@ path.  Heavy loops are in ``dm_oracle.c`` (built by ``oracle/Makefile`` into
   * ``filter_map``   Matching._filter         (misc/Matching.py:224-255)
   * ``match``        Matching.__call__ with _filter hooks (misc/Matching.py:80-149, 211-222)
   * ``cut_solve``    ImageCutSolver            (misc/image_cut_solver.py:26-184)
+  * ``atomic_patch`` Correlation_map._create_atomic_patch (misc/Correlation_map.py:51-67)
+  * ``bad_matching`` the row argmax of bad_matching.py:66-70
   * ``sub_pix_cal``  sub_pix_cal               (misc/sub_pix_cal.py:22-53)
   * ``optimize_loop``, ``make_weight``, ``opt_loop_bilateral``: the Gauss-Seidel loops of
     misc/optimize_loop.py:15-44 and misc/opt_loop.py:16-85 (loops in dm_oracle.c)
@@ -88,6 +90,30 @@ def corr_l0(img1, img2, ws, feature='cv2.TM_CCOEFF_NORMED'):
     if rc != 0:
         raise ValueError('dmo_corr_l0 failed: %d' % rc)
     return out
+
+
+def atomic_patch(img, ws):
+    """Correlation_map._create_atomic_patch (misc/Correlation_map.py:51-67): the overlapping
+    ws x ws patch at every pixel of the trimmed image, (h0, w0, ws, ws) uint8."""
+    img = np.asarray(img)
+    e = (ws - 1) // 2
+    H, W = img.shape
+    out = np.empty((H - 2 * e, W - 2 * e, ws, ws))
+    for i in range(e, H - e):
+        for j in range(e, W - e):
+            out[i - e, j - e] = img[i - e:i + e + 1, j - e:j + e + 1]
+    return out.astype(np.uint8)
+
+
+def bad_matching(l0):
+    """bad_matching.py:66-70: dis[i, j] = j - argmax(co_map[i, j, i, :]) on the level-0
+    min-max volume (pre-rectification); np.argmax takes the first maximum (first NaN)."""
+    h0, w0 = l0.shape[:2]
+    dis = np.zeros((h0, w0))
+    for i in range(h0):
+        for j in range(w0):
+            dis[i, j] = j - np.argmax(l0[i, j, i, :])
+    return dis
 
 
 def pyramid(l0):
@@ -235,11 +261,11 @@ def cut_solve(img1, img2, image_size=(32, 32), stride=(32, 32), window_size=5,
     (np.empty in the reference) are NaN here."""
     ex = int((window_size - 1) / 2)
     trimmed = [image_size[i] + 2 * ex for i in range(2)]
+    shape = img1.shape   # self.img_shape, recorded before _padding (:46) and used by :62
     if padding:  # _padding (:73-93): img1 copied twice, img2 left zero
         a = np.zeros((img1.shape[0] + 2 * ex, img1.shape[1] + 2 * ex))
         a[ex:-ex, ex:-ex] = img1
         img1, img2 = a.astype(np.uint8), np.zeros(a.shape, dtype=np.uint8)
-    shape = img1.shape
     n = [int(np.floor((shape[i] - trimmed[i]) / stride[i])) for i in range(2)]
     tiles = [(i, j) for j in range(n[1]) for i in range(n[0])]
     size = [stride[i] * tiles[-1][i] + image_size[i] for i in range(2)]

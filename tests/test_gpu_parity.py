@@ -125,11 +125,12 @@ def test_private_methods(case, mirror):
     _same(co._rectification(ol0), olev[0])
 
 
-@pytest.mark.parametrize('name', ['cut_44_s16_st12', 'cut_52x40_s16_pad'])
+@pytest.mark.parametrize('name', ['cut_44_s16_st12', 'cut_52x40_s16_pad', 'cut_48_s16_pad'])
 def test_image_cut_solver(name):
     from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
     g = np.load(os.path.join(GOLD, name + '.npz'))
-    modes = ['elevation', 'elevation2', 'distance'][:g['d_map'].shape[0]]
+    modes = ([str(m) for m in g['modes']] if 'modes' in g
+             else ['elevation', 'elevation2', 'distance'][:g['d_map'].shape[0]])
     pad = name.endswith('_pad')
     kw = dict(image_size=list(g['image_size']), stride=list(g['stride']), window_size=int(g['ws']),
               degree_map_mode=modes, padding=pad)
@@ -140,6 +141,27 @@ def test_image_cut_solver(name):
     covered = ~np.isnan(score)
     _close(d_map[:, covered], g['d_map'][:, covered], TOL_SUBPIX)
     _close(score[covered], g['score'][covered], TOL_F64)
+
+
+@pytest.mark.parametrize('path', sorted(glob.glob(os.path.join(GOLD, 'bad_matching_*.npz'))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_bad_matching_sequence(path, mirror):
+    """bad_matching.py:60-70 through the mirror: _create_atomic_patch() ->
+    _create_simple_initial_co_map() -> j - argmax co_map[i, j, i, :], bit-exact against the
+    reference's own output; atomic_patch too."""
+    CM, MT, CD = mirror
+    g = np.load(path)
+    co = CM.Correlation_map(g['img1'], g['img2'], window_size=int(g['ws']),
+                            feature_name=str(g['feature']))
+    co._create_atomic_patch()
+    _same(co.atomic_patch, g['atomic_patch'])
+    co._create_simple_initial_co_map()
+    dis = np.zeros((co.co_map.shape[0], co.co_map.shape[1]))
+    for i in range(co.co_map.shape[0]):
+        for j in range(co.co_map.shape[1]):
+            dis[i, j] = j - np.argmax(co.co_map[i, j, i, :])
+    _same(dis, g['dis'])
+    _same(co.co_map.astype(np.float32), O.corr_l0(g['img1'], g['img2'], int(g['ws']), str(g['feature'])))
 
 
 def test_sub_pix_cal():

@@ -102,3 +102,45 @@ def test_loader_channels(tmp_path):
     a, b = Loader([str(tmp_path / 'g1.png'), str(tmp_path / 'g2.png')], start=[1, 2], size=[8, 9],
                   integrated=False)()
     assert np.array_equal(a, g[1:9, 2:11]) and np.array_equal(b, g[::-1][1:9, 2:11])
+
+
+def test_alias_misc_imports_every_mirror_module():
+    """Reference scripts import ``misc.<module>`` (deep_dem_mathing.py:11-13,
+    optimize_looper.py:21 ``from misc.opt_loop import *``); under alias_misc() every module
+    of the reference's misc/ that the mirror re-provides must import, in a fresh
+    interpreter (no GPU needed to import)."""
+    import subprocess
+    import sys
+    code = ('import deepmatching_stereo_matching_amd as p; p.alias_misc()\n'
+            'from misc.opt_loop import *\n'
+            'from misc.optimize_loop import optimize_loop, image_threshold\n'
+            'from misc.Correlation_map import Correlation_map, Maxpool\n'
+            'from misc.Matching import Matching, Zero_padding\n'
+            'from misc.Calc_difference import Calc_difference\n'
+            'from misc.Feature_value import Feature_value\n'
+            'from misc.image_cut_solver import ImageCutSolver\n'
+            'from misc.loader import Loader\n'
+            'from misc.raw_read import RawRead\n'
+            'from misc.sub_pix_cal import sub_pix_cal\n'
+            'assert callable(make_weight) and callable(optimize_loop_bilateral_horizon)\n')
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, '-c', code], cwd=repo, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_atomic_patch_on_host_matches_reference():
+    """Correlation_map._create_atomic_patch runs on the host (no device needed) and equals
+    the reference's atomic_patch (bad_matching_* fixtures, Correlation_map.py:51-67)."""
+    import glob
+    from deepmatching_stereo_matching_amd.misc.Correlation_map import Correlation_map
+    paths = sorted(glob.glob(os.path.join(os.path.dirname(__file__), 'golden', 'bad_matching_*.npz')))
+    assert paths
+    for p in paths:
+        g = np.load(p)
+        co = Correlation_map(g['img1'], g['img2'], window_size=int(g['ws']),
+                             feature_name=str(g['feature']))
+        co._create_atomic_patch()
+        assert co.atomic_patch.dtype == np.uint8
+        assert np.array_equal(co.atomic_patch, g['atomic_patch'])
+        with pytest.raises(AttributeError):      # no co_map before _create_simple_initial_co_map
+            co.co_map

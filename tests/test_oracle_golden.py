@@ -104,10 +104,20 @@ def test_match_filtered(case):
             _close(m, g['match_filter_' + fm], TOL_SUBPIX)
 
 
-@pytest.mark.parametrize('name', ['cut_44_s16_st12', 'cut_52x40_s16_pad'])
+CUTS = ['cut_44_s16_st12', 'cut_52x40_s16_pad', 'cut_48_s16_pad']
+BAD = sorted(glob.glob(os.path.join(GOLD, 'bad_matching_*.npz')))
+
+
+def cut_modes(g):
+    if 'modes' in g:
+        return [str(m) for m in g['modes']]
+    return ['elevation', 'elevation2', 'distance'][:g['d_map'].shape[0]]
+
+
+@pytest.mark.parametrize('name', CUTS)
 def test_image_cut_solver(name):
     g = np.load(os.path.join(GOLD, name + '.npz'))
-    modes = ['elevation', 'elevation2', 'distance'][:g['d_map'].shape[0]]
+    modes = cut_modes(g)
     pad = name.endswith('_pad')
     d_map, score = O.cut_solve(g['img1'], g['img2'], image_size=list(g['image_size']),
                                stride=list(g['stride']), window_size=int(g['ws']),
@@ -123,3 +133,22 @@ def test_sub_pix_cal_py():
     _close(O.sub_pix_cal(g['arr'], g['co_map'], direction=0), g['out_dir0'], TOL_SUBPIX)
     _close(O.sub_pix_cal(g['arr'], g['co_map'], direction=1, ratio=30.), g['out_dir1'],
            TOL_SUBPIX)
+
+
+@pytest.mark.parametrize('path', BAD, ids=lambda p: os.path.basename(p)[:-4])
+def test_atomic_patch_and_bad_matching(path):
+    """_create_atomic_patch (Correlation_map.py:51-67) and bad_matching.py:60-70's row
+    argmax on the level-0 volume, against the reference's own outputs (bit-exact)."""
+    g = np.load(path)
+    ws, feat = int(g['ws']), str(g['feature'])
+    ap = O.atomic_patch(g['img1'], ws)
+    assert ap.dtype == g['atomic_patch'].dtype and np.array_equal(ap, g['atomic_patch'])
+    dis = O.bad_matching(O.corr_l0(g['img1'], g['img2'], ws, feat))
+    assert np.array_equal(dis, g['dis'])
+
+
+def test_padding_grid_counts_unpadded_shape():
+    """ImageCutSolver counts tiles on the image shape recorded before _padding
+    (image_cut_solver.py:46,62): 48x48, S=16 -> one tile, not the padded 52x52's 2x2."""
+    g = np.load(os.path.join(GOLD, 'cut_48_s16_pad.npz'))
+    assert g['d_map'].shape[1:] == (16, 16)
