@@ -98,7 +98,10 @@ class DevicePyramid:
     def __init__(self, batch, stream=None, build=True, fuse_level2=None):
         self.b = batch
         self.lib = L.load()
-        self.nlev, self.N_map = pyramid_plan(batch.h0, batch.w0)
+        try:   # a shape the pyramid rejects can still give its level-0 volume (bad_matching.py)
+            self._plan = pyramid_plan(batch.h0, batch.w0)
+        except ValueError as e:
+            self._plan = e
         self.stream = stream
         self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
                                  device=batch.device)
@@ -114,6 +117,20 @@ class DevicePyramid:
 
     def _s(self):
         return L.stream_handle(self.stream)
+
+    @property
+    def nlev(self):
+        """Level count (Correlation_map.iteration); raises the reference's aggregation
+        error for shapes whose sides do not halve down to the top level."""
+        if isinstance(self._plan, Exception):
+            raise self._plan
+        return self._plan[0]
+
+    @property
+    def N_map(self):
+        if isinstance(self._plan, Exception):
+            raise self._plan
+        return self._plan[1]
 
     def compute_stats(self):
         if not self._have_stats:

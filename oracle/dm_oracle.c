@@ -38,74 +38,135 @@
 #define DMO_CCOEFF 4 /* cv2.TM_CCOEFF */
 
 /* ---- level 0 -------------------------------------------------------------------- */
-/* img/tmpl: uint8 H x W row-major.  l0: [h0*w0][h0*w0] float32, h0 = H-ws+1. */
-int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
-                int method, float *l0)
+/* Per-window sums of the template image: sI[q] = sum(I), bq[q] = f32(1/sqrt(f64 dI)). */
+typedef struct {
+    const uint8_t *img, *tmpl;
+    int W, ws, h0, w0, method;
+    int64_t *sI;
+    float *bq;
+} l0_src;
+
+static int l0_init(l0_src *s, const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
+                   int method)
 {
     if (ws < 1 || (ws & 1) == 0 || H < ws || W < ws || ws > 21) return -1;
     if (method != DMO_NORMED && method != DMO_CCOEFF) return -2;
-    const int h0 = H - ws + 1, w0 = W - ws + 1, n = ws * ws;
-    const long P = (long)h0 * w0;
-    int64_t *sI = malloc(sizeof(int64_t) * P);
-    float *bq = malloc(sizeof(float) * P);
-    for (int q0 = 0; q0 < h0; ++q0)
-        for (int q1 = 0; q1 < w0; ++q1) {
-            int64_t s = 0, s2 = 0;
+    s->img = img; s->tmpl = tmpl; s->W = W; s->ws = ws; s->method = method;
+    s->h0 = H - ws + 1; s->w0 = W - ws + 1;
+    const int n = ws * ws;
+    const long P = (long)s->h0 * s->w0;
+    s->sI = malloc(sizeof(int64_t) * P);
+    s->bq = malloc(sizeof(float) * P);
+    for (int q0 = 0; q0 < s->h0; ++q0)
+        for (int q1 = 0; q1 < s->w0; ++q1) {
+            int64_t a = 0, a2 = 0;
             for (int u = 0; u < ws; ++u)
                 for (int v = 0; v < ws; ++v) {
                     int64_t x = tmpl[(long)(q0 + u) * W + q1 + v];
-                    s += x; s2 += x * x;
+                    a += x; a2 += x * x;
                 }
-            long q = (long)q0 * w0 + q1;
-            int64_t dI = (int64_t)n * s2 - s * s;
-            sI[q] = s;
-            bq[q] = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
+            long q = (long)q0 * s->w0 + q1;
+            int64_t dI = (int64_t)n * a2 - a * a;
+            s->sI[q] = a;
+            s->bq[q] = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
         }
+    return 0;
+}
+
+static void l0_free(l0_src *s) { free(s->sI); free(s->bq); }
+
+/* Row p of the level-0 volume: Feature_value(patch p, template) = matchTemplate with the
+ * pinned formula (oracle/cv2_shim/cv2.py), then min_max (misc/Feature_value.py:32-43), in
+ * float32.  acc: w0 int32 scratch.  sum(T*I) <= 21*21*255*255 fits int32 exactly. */
+static void l0_row(const l0_src *s, long p, float *row, int32_t *acc)
+{
+    const int ws = s->ws, W = s->W, h0 = s->h0, w0 = s->w0, n = ws * ws;
+    const long P = (long)h0 * w0;
+    const int p0 = (int)(p / w0), p1 = (int)(p % w0);
+    int T[21 * 21];
+    int64_t sT = 0, sT2 = 0;
+    for (int u = 0; u < ws; ++u)
+        for (int v = 0; v < ws; ++v) {
+            int x = s->img[(long)(p0 + u) * W + p1 + v];
+            T[u * ws + v] = x; sT += x; sT2 += (int64_t)x * x;
+        }
+    const int64_t dT = (int64_t)n * sT2 - sT * sT;
+    const float a = dT == 0 ? 0.0f : (float)(1.0 / sqrt((double)dT));
     const float inv_n = (float)(1.0 / n);
-    #pragma omp parallel for schedule(dynamic, 1)
-    for (long p = 0; p < P; ++p) {
-        const int p0 = (int)(p / w0), p1 = (int)(p % w0);
-        int T[15 * 15 + 256];
-        int64_t sT = 0, sT2 = 0;
+    for (int q0 = 0; q0 < h0; ++q0) {
+        for (int q1 = 0; q1 < w0; ++q1) acc[q1] = 0;
         for (int u = 0; u < ws; ++u)
             for (int v = 0; v < ws; ++v) {
-                int x = img[(long)(p0 + u) * W + p1 + v];
-                T[u * ws + v] = x; sT += x; sT2 += (int64_t)x * x;
+                const int32_t t = T[u * ws + v];
+                const uint8_t *ir = s->tmpl + (long)(q0 + u) * W + v;
+                for (int q1 = 0; q1 < w0; ++q1) acc[q1] += t * (int32_t)ir[q1];
             }
-        float *row = l0 + p * P;
-        const int64_t dT = (int64_t)n * sT2 - sT * sT;
-        const float a = dT == 0 ? 0.0f : (float)(1.0 / sqrt((double)dT));
-        for (int q0 = 0; q0 < h0; ++q0)
-            for (int q1 = 0; q1 < w0; ++q1) {
-                const long q = (long)q0 * w0 + q1;
-                int64_t sTI = 0;
-                for (int u = 0; u < ws; ++u) {
-                    const uint8_t *ir = tmpl + (long)(q0 + u) * W + q1;
-                    for (int v = 0; v < ws; ++v) sTI += (int64_t)T[u * ws + v] * ir[v];
-                }
-                const int64_t num = (int64_t)n * sTI - sT * sI[q];
-                float r;
-                if (method == DMO_CCOEFF) {
-                    r = (float)num * inv_n;
-                } else if (dT == 0) {
-                    r = 1.0f;
-                } else {
-                    const float y = (float)num * bq[q];
-                    r = y * a;
-                    r = r < -1.0f ? -1.0f : (r > 1.0f ? 1.0f : r);
-                }
-                row[q] = r;
+        float *o = row + (long)q0 * w0;
+        for (int q1 = 0; q1 < w0; ++q1) {
+            const long q = (long)q0 * w0 + q1;
+            const int64_t num = (int64_t)n * acc[q1] - sT * s->sI[q];
+            float r;
+            if (s->method == DMO_CCOEFF) {
+                r = (float)num * inv_n;
+            } else if (dT == 0) {
+                r = 1.0f;
+            } else {
+                const float y = (float)num * s->bq[q];
+                r = y * a;
+                r = r < -1.0f ? -1.0f : (r > 1.0f ? 1.0f : r);
             }
-        /* Feature_value.min_max: (x - min) / (max - min) in float32 */
-        float mn = row[0], mx = row[0];
-        for (long q = 1; q < P; ++q) {
-            if (row[q] < mn) mn = row[q];
-            if (row[q] > mx) mx = row[q];
+            o[q1] = r;
         }
-        const float den = mx - mn;
-        for (long q = 0; q < P; ++q) row[q] = (row[q] - mn) / den;
     }
-    free(sI); free(bq);
+    /* Feature_value.min_max: (x - min) / (max - min) in float32 */
+    float mn = row[0], mx = row[0];
+    for (long q = 1; q < P; ++q) {
+        if (row[q] < mn) mn = row[q];
+        if (row[q] > mx) mx = row[q];
+    }
+    const float den = mx - mn;
+    for (long q = 0; q < P; ++q) row[q] = (row[q] - mn) / den;
+}
+
+/* img/tmpl: uint8 H x W row-major.  l0: [h0*w0][h0*w0] float32, h0 = H-ws+1.
+ * Correlation_map._create_atomic_patch + _create_simple_initial_co_map (:51-87). */
+int dmo_corr_l0(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
+                int method, float *l0)
+{
+    l0_src s;
+    int rc = l0_init(&s, img, tmpl, H, W, ws, method);
+    if (rc) return rc;
+    const long P = (long)s.h0 * s.w0;
+    #pragma omp parallel
+    {
+        int32_t *acc = malloc(sizeof(int32_t) * s.w0);
+        #pragma omp for schedule(dynamic, 1)
+        for (long p = 0; p < P; ++p) l0_row(&s, p, l0 + p * P, acc);
+        free(acc);
+    }
+    l0_free(&s);
+    return 0;
+}
+
+/* Rows of selected patches only (out: [n][P] float32): the level-0 values the C5 tests
+ * sample from an S = 256 tile without materialising its 17 GB volume. */
+int dmo_corr_l0_rows(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws, int method,
+                     const int64_t *patches, long n, float *out)
+{
+    l0_src s;
+    int rc = l0_init(&s, img, tmpl, H, W, ws, method);
+    if (rc) return rc;
+    const long P = (long)s.h0 * s.w0;
+    for (long k = 0; k < n; ++k)
+        if (patches[k] < 0 || patches[k] >= P) { l0_free(&s); return -3; }
+    #pragma omp parallel
+    {
+        int32_t *acc = malloc(sizeof(int32_t) * s.w0);
+        #pragma omp for schedule(dynamic, 1)
+        for (long k = 0; k < n; ++k) l0_row(&s, patches[k], out + k * P, acc);
+        free(acc);
+    }
+    l0_free(&s);
     return 0;
 }
 
@@ -218,14 +279,41 @@ static double sub_pix_compute(double r0, double r1, double r_)
     return 0;
 }
 
-/* levels[l]: (h0>>l, w0>>l, h0>>l, w0>>l) f64 rectified.  out: (3, h0, w0) f64. */
-int dmo_match(const double *const *levels, int nlev, int h0, int w0, int sub_pix,
-              double *out)
+/* Matching._sub_pix_cal for one pixel (misc/Matching.py:177-209) on its rectified level-0
+ * map M (h0 x w0): rows, then columns; index -1 wraps (python), index h0 / w0 raises
+ * IndexError -> bare except -> no change. */
+static void sub_pix_one(const double *M, int h0, int w0, int i, int j, double *m0, double *m1)
 {
-    if (nlev < 2) return -1; /* Matching._B indexes co_map_list[-2] unconditionally */
+    const int c0 = (int)*m0, c1 = (int)*m1;
+    const double d_x = i - *m0;
+    if (c0 + 1 >= h0) {
+        *m0 = i - d_x;                                   /* IndexError branch */
+    } else {
+        const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1;     /* python wraps -1 */
+        const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)(c0 + 1) * w0 + c1],
+                     r_ = M[(long)cm * w0 + c1];
+        *m0 = i - d_x + sub_pix_compute(r0, r1, r_);
+    }
+    const double d_y = j - *m1;
+    if (c1 + 1 >= w0) {
+        *m1 = j - d_y;
+    } else {
+        const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
+        const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)c0 * w0 + c1 + 1],
+                     r_ = M[(long)c0 * w0 + cm];
+        *m1 = j - d_y + sub_pix_compute(r0, r1, r_);
+    }
+}
+
+static const int OFF[4][2] = {{1, 1}, {0, 1}, {1, 0}, {0, 0}};   /* _B's o order (:111) */
+
+/* _initial_move_map + _B down to level `stop` (misc/Matching.py:80-149); cur holds the
+ * (3, h, w) map of level `stop` on return.  levels[l] for l >= stop must be present. */
+static void descend(const double *const *levels, int nlev, int h0, int w0, int stop,
+                    double **pcur, double **pnxt)
+{
+    double *cur = *pcur, *nxt = *pnxt;
     int h = h0 >> (nlev - 1), w = w0 >> (nlev - 1);
-    double *cur = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
-    double *nxt = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
     const double *L = levels[nlev - 1];
     long P = (long)h * w;
     for (int i = 0; i < h; ++i)
@@ -234,8 +322,7 @@ int dmo_match(const double *const *levels, int nlev, int h0, int w0, int sub_pix
             near_match(L + ((long)i * w + j) * P, h, w, i, j, o);
             for (int k = 0; k < 3; ++k) cur[k * P + (long)i * w + j] = o[k];
         }
-    static const int OFF[4][2] = {{1, 1}, {0, 1}, {1, 0}, {0, 0}};
-    for (int l = nlev - 2; l >= 0; --l) {
+    for (int l = nlev - 2; l >= stop; --l) {
         const int hn = h * 2, wn = w * 2;
         const long Pn = (long)hn * wn;
         L = levels[l];
@@ -254,35 +341,130 @@ int dmo_match(const double *const *levels, int nlev, int h0, int w0, int sub_pix
         double *t = cur; cur = nxt; nxt = t;
         h = hn; w = wn; P = Pn;
     }
-    if (sub_pix) {
-        const double *L0 = levels[0];
+    *pcur = cur; *pnxt = nxt;
+}
+
+/* levels[l]: (h0>>l, w0>>l, h0>>l, w0>>l) f64 rectified.  out: (3, h0, w0) f64. */
+int dmo_match(const double *const *levels, int nlev, int h0, int w0, int sub_pix,
+              double *out)
+{
+    if (nlev < 2) return -1; /* Matching._B indexes co_map_list[-2] unconditionally */
+    double *cur = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
+    double *nxt = malloc(sizeof(double) * 3 * (size_t)h0 * w0);
+    descend(levels, nlev, h0, w0, 0, &cur, &nxt);
+    const long P = (long)h0 * w0;
+    if (sub_pix)
         for (int i = 0; i < h0; ++i)
             for (int j = 0; j < w0; ++j) {
                 const long pc = (long)i * w0 + j;
-                const double *M = L0 + pc * P;
-                const int c0 = (int)cur[pc], c1 = (int)cur[P + pc];
-                const double d_x = i - cur[pc];
-                if (c0 + 1 >= h0) {
-                    cur[pc] = i - d_x;                       /* IndexError branch */
-                } else {
-                    const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1; /* python wraps -1 */
-                    const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)(c0 + 1) * w0 + c1],
-                                 r_ = M[(long)cm * w0 + c1];
-                    cur[pc] = i - d_x + sub_pix_compute(r0, r1, r_);
-                }
-                const double d_y = j - cur[P + pc];
-                if (c1 + 1 >= w0) {
-                    cur[P + pc] = j - d_y;
-                } else {
-                    const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
-                    const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)c0 * w0 + c1 + 1],
-                                 r_ = M[(long)c0 * w0 + cm];
-                    cur[P + pc] = j - d_y + sub_pix_compute(r0, r1, r_);
-                }
+                sub_pix_one(levels[0] + pc * P, h0, w0, i, j, &cur[pc], &cur[P + pc]);
             }
-    }
     memcpy(out, cur, sizeof(double) * 3 * P);
     free(cur); free(nxt);
+    return 0;
+}
+
+/* ---- streaming mode: tiles whose level 0 does not fit in host memory (C5, S = 256) ---- *
+ * The same arithmetic in the same order as dmo_corr_l0 -> pyramid -> dmo_match, but level 0
+ * is never stored: each level-1 cell recomputes its four children's level-0 rows, rectifies
+ * them (_rectification, :158-159), max-pools them (:101-103) and averages the four pooled
+ * maps (:109-122) before the cell's own rectification (:148); the last descent step of
+ * Matching (level 0) and the sub-pixel fit recompute each pixel's level-0 row. */
+
+/* rectified level-0 row of patch p: x[q] = rect(min-max ZNCC) as float64 */
+static void l0_row_rect(const l0_src *s, long p, double lam, float *row, double *x, int32_t *acc)
+{
+    const long P = (long)s->h0 * s->w0;
+    l0_row(s, p, row, acc);
+    for (long q = 0; q < P; ++q) x[q] = rect((double)row[q], lam);
+}
+
+/* level 1 (rectified): l1 [(h0/2)(w0/2)][(h0/2)(w0/2)] float64 */
+int dmo_corr_level1_stream(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
+                           int method, double lam, double *l1)
+{
+    l0_src s;
+    int rc = l0_init(&s, img, tmpl, H, W, ws, method);
+    if (rc) return rc;
+    const int h0 = s.h0, w0 = s.w0, h1 = h0 / 2, w1 = w0 / 2;
+    if ((h0 & 1) || (w0 & 1)) { l0_free(&s); return -4; }
+    const long P = (long)h0 * w0, P1 = (long)h1 * w1;
+    #pragma omp parallel
+    {
+        int32_t *acc = malloc(sizeof(int32_t) * w0);
+        float *row = malloc(sizeof(float) * P);
+        double *x = malloc(sizeof(double) * P);
+        double *R = malloc(sizeof(double) * 4 * P1);
+        #pragma omp for schedule(dynamic, 1)
+        for (long c = 0; c < P1; ++c) {
+            const int i = (int)(c / w1), j = (int)(c % w1);
+            /* children in the reference's summation order: ul, ur, ll, lr */
+            const long child[4] = {(long)(2 * i) * w0 + 2 * j, (long)(2 * i) * w0 + 2 * j + 1,
+                                   (long)(2 * i + 1) * w0 + 2 * j, (long)(2 * i + 1) * w0 + 2 * j + 1};
+            for (int k = 0; k < 4; ++k) {
+                l0_row_rect(&s, child[k], lam, row, x, acc);
+                double *r = R + k * P1;
+                for (int u = 0; u < h1; ++u)
+                    for (int v = 0; v < w1; ++v) {
+                        double m = -INFINITY;
+                        for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+                            if (a < 0 || a >= h0) continue;
+                            for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                                if (b < 0 || b >= w0) continue;
+                                m = nanmax(m, x[(long)a * w0 + b]);
+                            }
+                        }
+                        r[(long)u * w1 + v] = m;
+                    }
+            }
+            double *o = l1 + c * P1;
+            for (long k = 0; k < P1; ++k)
+                o[k] = rect((R[k] + R[P1 + k] + R[2 * P1 + k] + R[3 * P1 + k]) / 4, lam);
+        }
+        free(acc); free(row); free(x); free(R);
+    }
+    l0_free(&s);
+    return 0;
+}
+
+/* Matching()() with level 0 recomputed: levels[0] is ignored (may be NULL), levels[1..] as
+ * dmo_match.  out: (3, h0, w0) f64. */
+int dmo_match_stream(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws, int method,
+                     double lam, const double *const *levels, int nlev, int sub_pix, double *out)
+{
+    if (nlev < 2) return -1;
+    l0_src s;
+    int rc = l0_init(&s, img, tmpl, H, W, ws, method);
+    if (rc) return rc;
+    const int h0 = s.h0, w0 = s.w0, h1 = h0 / 2, w1 = w0 / 2;
+    const long P = (long)h0 * w0, P1 = (long)h1 * w1;
+    double *cur = malloc(sizeof(double) * 3 * (size_t)P);
+    double *nxt = malloc(sizeof(double) * 3 * (size_t)P);
+    descend(levels, nlev, h0, w0, 1, &cur, &nxt);           /* level-1 map in cur */
+    #pragma omp parallel
+    {
+        int32_t *acc = malloc(sizeof(int32_t) * w0);
+        float *row = malloc(sizeof(float) * P);
+        double *x = malloc(sizeof(double) * P);
+        #pragma omp for schedule(dynamic, 1)
+        for (long pc = 0; pc < P1; ++pc) {
+            const int i = (int)(pc / w1), j = (int)(pc % w1);
+            const int64_t b0 = (int64_t)(cur[pc] * 2), b1 = (int64_t)(cur[P1 + pc] * 2);
+            for (int k = 0; k < 4; ++k) {
+                const int p0 = 2 * i + OFF[k][0], p1 = 2 * j + OFF[k][1];
+                const long p = (long)p0 * w0 + p1;
+                l0_row_rect(&s, p, lam, row, x, acc);
+                double o[3];
+                near_match(x, h0, w0, (int)(b0 + OFF[k][0]), (int)(b1 + OFF[k][1]), o);
+                if (sub_pix) sub_pix_one(x, h0, w0, p0, p1, &o[0], &o[1]);
+                for (int c = 0; c < 3; ++c) nxt[c * P + p] = o[c];
+            }
+        }
+        free(acc); free(row); free(x);
+    }
+    memcpy(out, nxt, sizeof(double) * 3 * P);
+    free(cur); free(nxt);
+    l0_free(&s);
     return 0;
 }
 

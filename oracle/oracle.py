@@ -9,6 +9,8 @@ path.  Heavy loops are in ``dm_oracle.c`` (built by ``oracle/Makefile`` into
   * ``match``        Matching.__call__ with _filter hooks (misc/Matching.py:80-149, 211-222)
   * ``cut_solve``    ImageCutSolver            (misc/image_cut_solver.py:26-184)
   * ``atomic_patch`` Correlation_map._create_atomic_patch (misc/Correlation_map.py:51-67)
+  * ``pyramid_stream`` / ``match_stream`` / ``corr_l0_rows``: the same pipeline without
+    storing level 0 (C5 tiles, S = 256, whose float64 level 0 is 34 GB; dm_oracle.c)
   * ``bad_matching`` the row argmax of bad_matching.py:66-70
   * ``sub_pix_cal``  sub_pix_cal               (misc/sub_pix_cal.py:22-53)
   * ``optimize_loop``, ``make_weight``, ``opt_loop_bilateral``: the Gauss-Seidel loops of
@@ -45,6 +47,12 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.dmo_corr_l0.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        L.dmo_corr_l0_rows.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       P, ctypes.c_long, P]
+        L.dmo_corr_level1_stream.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_double, P]
+        L.dmo_match_stream.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_double, P, ctypes.c_int, ctypes.c_int, P]
         L.dmo_rectify_f32.argtypes = [P, ctypes.c_long, ctypes.c_double, P]
         L.dmo_rectify_f64.argtypes = [P, ctypes.c_long, ctypes.c_double]
         L.dmo_aggregate.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
@@ -89,6 +97,76 @@ def corr_l0(img1, img2, ws, feature='cv2.TM_CCOEFF_NORMED'):
         rc = lib().dmo_corr_l0(_p(img1), _p(img2), H, W, ws, METHODS[feature], _p(out))
     if rc != 0:
         raise ValueError('dmo_corr_l0 failed: %d' % rc)
+    return out
+
+
+def corr_l0_rows(img1, img2, ws, patches, feature='cv2.TM_CCOEFF_NORMED'):
+    """Rows ``patches`` (flat p indices) of the level-0 volume: [n][h0*w0] float32, equal to
+    corr_l0(...).reshape(P, P)[patches] without materialising the volume."""
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    H, W = img1.shape
+    P = (H - ws + 1) * (W - ws + 1)
+    idx = np.ascontiguousarray(patches, dtype=np.int64).ravel()
+    out = np.empty((len(idx), P), dtype=np.float32)
+    with np.errstate(all='ignore'):
+        rc = lib().dmo_corr_l0_rows(_p(img1), _p(img2), H, W, ws, METHODS[feature], _p(idx),
+                                    len(idx), _p(out))
+    if rc != 0:
+        raise ValueError('dmo_corr_l0_rows failed: %d' % rc)
+    return out
+
+
+def pyramid_stream(img1, img2, ws, feature='cv2.TM_CCOEFF_NORMED'):
+    """Levels >= 1 of Correlation_map()() without storing level 0 (dmo_corr_level1_stream,
+    then the same aggregation as pyramid()): for tiles whose float64 level 0 does not fit
+    the host (C5: S = 256 is 34 GB).  Returns ([None, level1, ...], iteration, N_map);
+    bit-identical to pyramid(corr_l0(...)) levels >= 1."""
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    H, W = img1.shape
+    h0, w0 = H - ws + 1, W - ws + 1
+    if min(h0, w0) == 1:          # no aggregation at all (:145)
+        return [None], 1, 1
+    if h0 % 2 or w0 % 2:
+        raise ValueError('could not broadcast input array: map sides must halve '
+                         '(misc/Correlation_map.py:96-103)')
+    L = lib()
+    cur = np.empty((h0 // 2, w0 // 2, h0 // 2, w0 // 2), dtype=np.float64)
+    with np.errstate(all='ignore'):
+        rc = L.dmo_corr_level1_stream(_p(img1), _p(img2), H, W, ws, METHODS[feature], LAM, _p(cur))
+    if rc != 0:
+        raise ValueError('dmo_corr_level1_stream failed: %d' % rc)
+    levels, N, it = [None, cur], 2, 2
+    while N < min(h0, w0):
+        h, w = cur.shape[:2]
+        if h % 2 or w % 2:
+            raise ValueError('could not broadcast input array: map sides must halve '
+                             '(misc/Correlation_map.py:96-103)')
+        nxt = np.empty((h // 2, w // 2, h // 2, w // 2), dtype=np.float64)
+        L.dmo_aggregate(_p(cur), h, w, _p(nxt))
+        L.dmo_rectify_f64(_p(nxt), nxt.size, LAM)
+        levels.append(nxt)
+        cur = nxt
+        N *= 2
+        it += 1
+    return levels, it, N
+
+
+def match_stream(img1, img2, ws, levels, sub_pix=True, feature='cv2.TM_CCOEFF_NORMED'):
+    """Matching()() with level 0 recomputed per pixel (dmo_match_stream); levels[0] unused.
+    Bit-identical to match(pyramid(corr_l0(...))[0], sub_pix)."""
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    H, W = img1.shape
+    h0, w0 = H - ws + 1, W - ws + 1
+    ptrs = (ctypes.c_void_p * len(levels))(*[None if lv is None else lv.ctypes.data for lv in levels])
+    out = np.empty((3, h0, w0), dtype=np.float64)
+    with np.errstate(all='ignore'):
+        rc = lib().dmo_match_stream(_p(img1), _p(img2), H, W, ws, METHODS[feature], LAM, ptrs,
+                                    len(levels), int(bool(sub_pix)), _p(out))
+    if rc != 0:
+        raise IndexError('list index out of range (Matching._B needs >= 2 levels)')
     return out
 
 
