@@ -22,6 +22,7 @@ DEPS = SOURCES + [os.path.join(CSRC, f) for f in ('dm_pow.h', 'dm_pow_tables.h',
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 FLAGS = ['-O3', '-std=c++17', '-ffp-contract=off', '-fPIC', '-shared', '-Wno-pass-failed',
+         '-mllvm', '-amdgpu-mfma-vgpr-form',  # MFMA C/D in VGPRs: no v_accvgpr copies per tile
          '--offload-arch=%s' % ARCH, '-I', os.path.join(REPO, 'include')]
 
 

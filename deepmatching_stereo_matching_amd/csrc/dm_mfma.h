@@ -115,10 +115,15 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
 
 // y = f32(num) * b_q for the 4 patches (acc[r]) of one lane against its window (qs).
 // YF (n <= 25): acc was accumulated onto DM_YBIAS, so its bits read as the float
-// 1.5*2^23 + acc (exact for |acc| <= 128^2 n < 2^22); with sTf = f32(sum T') and
-// -sum(I') = f32 bits in qs.x, sT*sI is exact in f32 (|.| <= (128 n)^2 < 2^24) and
-// fma(acc, n, -sT sI) rounds the exact integer num once -- the same f32(num) as the
-// integer path, in packed-f32 instructions (2 voxels each).
+// A = 1.5*2^23 + acc (exact for |acc| <= 128^2 n < 2^22).  Three packed-f32 steps, each
+// exact or rounding an exact integer once:
+//   m   = fma(A, n, -n*1.5*2^23)  = n*acc        exact: |n acc| <= 128^2 n^2 < 2^24, and
+//                                                -n*1.5*2^23 = -3n*2^22 is an f32 (3n <= 75)
+//   num = fma(sT, -sI, m)         = n*acc - sT*sI, exact: |num| <= sqrt(dT dI) <= n^2 255^2/4
+//                                                < 2^24 (Cauchy-Schwarz)
+//   y   = num * b_q               the one rounding of the reference's f32(num) * b_q
+// (sTf = f32(sum T'), qs.x = f32 bits of -sum(I')) -- the integer path's f32(num) in 1.5
+// packed instructions per voxel instead of 2.
 #define DM_YBIAS 0x4B400000
 typedef float dm_f2 __attribute__((ext_vector_type(2)));
 
@@ -129,14 +134,13 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
     const float b = __int_as_float(qs.y);
     if constexpr (YF) {
         const float nf = (float)n, sI = __int_as_float(qs.x);
-        const dm_f2 bias = BF ? dm_f2{0.0f, 0.0f} : dm_f2{12582912.0f, 12582912.0f};
-        dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
-        dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
-        if constexpr (!BF) { a01 = a01 - bias; a23 = a23 - bias; }
-        const dm_f2 p01 = dm_f2{sTf[0], sTf[1]} * dm_f2{sI, sI};
-        const dm_f2 p23 = dm_f2{sTf[2], sTf[3]} * dm_f2{sI, sI};
-        const dm_f2 n01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, p01);
-        const dm_f2 n23 = __builtin_elementwise_fma(a23, dm_f2{nf, nf}, p23);
+        const float nb = BF ? 0.0f : -nf * 12582912.0f;   // exact (see above)
+        const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
+        const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
+        const dm_f2 m01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, dm_f2{nb, nb});
+        const dm_f2 m23 = __builtin_elementwise_fma(a23, dm_f2{nf, nf}, dm_f2{nb, nb});
+        const dm_f2 n01 = __builtin_elementwise_fma(dm_f2{sTf[0], sTf[1]}, dm_f2{sI, sI}, m01);
+        const dm_f2 n23 = __builtin_elementwise_fma(dm_f2{sTf[2], sTf[3]}, dm_f2{sI, sI}, m23);
         const dm_f2 y01 = n01 * dm_f2{b, b}, y23 = n23 * dm_f2{b, b};
         y[0] = y01.x; y[1] = y01.y; y[2] = y23.x; y[3] = y23.y;
     } else {
@@ -810,11 +814,20 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
             y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);
-                xs[tw][r] = norm_mk(rr, rmn[r], den[r], rinv[r]);
-            }
+            // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
+            const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
+            const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
+            const float rr[4] = {__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1]),
+                                 __builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
+            const dm_f2 a01 = dm_f2{rr[0], rr[1]} - dm_f2{rmn[0], rmn[1]};
+            const dm_f2 a23 = dm_f2{rr[2], rr[3]} - dm_f2{rmn[2], rmn[3]};
+            const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
+            const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
+            const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
+            const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
+            const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
+            const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
+            xs[tw][0] = x01.x; xs[tw][1] = x01.y; xs[tw][2] = x23.x; xs[tw][3] = x23.y;
         }
         const int col = 16 * GW * gg + GW * c;
 #pragma unroll
@@ -983,11 +996,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
             y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float rr = __builtin_amdgcn_fmed3f(__fmul_rn(y[r], ap[r]), lo[r], hi[r]);
-                xs[tw][r] = norm_mk(rr, rmn[r], den[r], rinv[r]);
-            }
+            // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
+            const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
+            const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
+            const float rr[4] = {__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1]),
+                                 __builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
+            const dm_f2 a01 = dm_f2{rr[0], rr[1]} - dm_f2{rmn[0], rmn[1]};
+            const dm_f2 a23 = dm_f2{rr[2], rr[3]} - dm_f2{rmn[2], rmn[3]};
+            const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
+            const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
+            const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
+            const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
+            const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
+            const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
+            xs[tw][0] = x01.x; xs[tw][1] = x01.y; xs[tw][2] = x23.x; xs[tw][3] = x23.y;
         }
         const int col = 16 * GW * wave + GW * c, slot = q0 % RB;
 #pragma unroll

@@ -41,10 +41,18 @@
 /* Per-window sums of the template image: sI[q] = sum(I), bq[q] = f32(1/sqrt(f64 dI)). */
 typedef struct {
     const uint8_t *img, *tmpl;
-    int W, ws, h0, w0, method;
-    int64_t *sI;
+    int W, ws, h0, w0, method, formula;
+    int64_t *sI, *dI;
     float *bq;
 } l0_src;
+
+/* ZNCC formula: 0 = the pinned one the kernels evaluate,
+ *   y = f32(num) * f32(1/sqrt(f64 dI)), r = clamp(y * f32(1/sqrt(f64 dT)));
+ * 1 = SURVEY.md 8(c)'s, r = f32(clamp(num / sqrt(f64 dT * f64 dI))) (OpenCV's double-
+ * precision division, one rounding).  1 exists only to MEASURE the difference
+ * (tools/zncc_pin.py); the goldens and every parity test use 0. */
+static int g_zncc = 0;
+void dmo_set_zncc_formula(int f) { g_zncc = f; }
 
 static int l0_init(l0_src *s, const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws,
                    int method)
@@ -52,10 +60,12 @@ static int l0_init(l0_src *s, const uint8_t *img, const uint8_t *tmpl, int H, in
     if (ws < 1 || (ws & 1) == 0 || H < ws || W < ws || ws > 21) return -1;
     if (method != DMO_NORMED && method != DMO_CCOEFF) return -2;
     s->img = img; s->tmpl = tmpl; s->W = W; s->ws = ws; s->method = method;
+    s->formula = g_zncc;
     s->h0 = H - ws + 1; s->w0 = W - ws + 1;
     const int n = ws * ws;
     const long P = (long)s->h0 * s->w0;
     s->sI = malloc(sizeof(int64_t) * P);
+    s->dI = malloc(sizeof(int64_t) * P);
     s->bq = malloc(sizeof(float) * P);
     for (int q0 = 0; q0 < s->h0; ++q0)
         for (int q1 = 0; q1 < s->w0; ++q1) {
@@ -68,12 +78,13 @@ static int l0_init(l0_src *s, const uint8_t *img, const uint8_t *tmpl, int H, in
             long q = (long)q0 * s->w0 + q1;
             int64_t dI = (int64_t)n * a2 - a * a;
             s->sI[q] = a;
+            s->dI[q] = dI;
             s->bq[q] = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
         }
     return 0;
 }
 
-static void l0_free(l0_src *s) { free(s->sI); free(s->bq); }
+static void l0_free(l0_src *s) { free(s->sI); free(s->dI); free(s->bq); }
 
 /* Row p of the level-0 volume: Feature_value(patch p, template) = matchTemplate with the
  * pinned formula (oracle/cv2_shim/cv2.py), then min_max (misc/Feature_value.py:32-43), in
@@ -110,6 +121,13 @@ static void l0_row(const l0_src *s, long p, float *row, int32_t *acc)
                 r = (float)num * inv_n;
             } else if (dT == 0) {
                 r = 1.0f;
+            } else if (s->formula == 1) {
+                if (s->dI[q] == 0) {
+                    r = 0.0f;
+                } else {
+                    double d = (double)num / sqrt((double)dT * (double)s->dI[q]);
+                    r = (float)(d < -1.0 ? -1.0 : (d > 1.0 ? 1.0 : d));
+                }
             } else {
                 const float y = (float)num * s->bq[q];
                 r = y * a;
@@ -167,6 +185,65 @@ int dmo_corr_l0_rows(const uint8_t *img, const uint8_t *tmpl, int H, int W, int 
         free(acc);
     }
     l0_free(&s);
+    return 0;
+}
+
+/* Distance between the two ZNCC formulas on one pair's level 0 (tools/zncc_pin.py):
+ * st[0] = values that differ, st[1] = max float32 ulp distance (finite values),
+ * st[2] = NaN positions that differ, st[3] = rows (patches) with any difference;
+ * max_abs = max |a - b| over finite values. */
+static long ulp_dist(float a, float b)
+{
+    int32_t ia, ib;
+    memcpy(&ia, &a, 4); memcpy(&ib, &b, 4);
+    if (ia < 0) ia = (int32_t)0x80000000 - ia;
+    if (ib < 0) ib = (int32_t)0x80000000 - ib;
+    long d = (long)ia - (long)ib;
+    return d < 0 ? -d : d;
+}
+
+int dmo_zncc_formula_diff(const uint8_t *img, const uint8_t *tmpl, int H, int W, int ws, int method,
+                          long *st, double *max_abs)
+{
+    l0_src s0, s1;
+    const int keep = g_zncc;
+    g_zncc = 0;
+    int rc = l0_init(&s0, img, tmpl, H, W, ws, method);
+    g_zncc = 1;
+    if (!rc) rc = l0_init(&s1, img, tmpl, H, W, ws, method);
+    g_zncc = keep;
+    if (rc) return rc;
+    const long P = (long)s0.h0 * s0.w0;
+    long nd = 0, mu = 0, nn = 0, rows = 0;
+    double ma = 0.0;
+    #pragma omp parallel reduction(+:nd, nn, rows) reduction(max:mu, ma)
+    {
+        int32_t *acc = malloc(sizeof(int32_t) * s0.w0);
+        float *a = malloc(sizeof(float) * P), *b = malloc(sizeof(float) * P);
+        #pragma omp for schedule(dynamic, 1)
+        for (long p = 0; p < P; ++p) {
+            l0_row(&s0, p, a, acc);
+            l0_row(&s1, p, b, acc);
+            long d_row = 0;
+            for (long q = 0; q < P; ++q) {
+                const int na = isnan(a[q]), nb = isnan(b[q]);
+                if (na || nb) { if (na != nb) { ++nn; ++d_row; } continue; }
+                if (a[q] != b[q]) {
+                    ++d_row;
+                    const long u = ulp_dist(a[q], b[q]);
+                    if (u > mu) mu = u;
+                    const double ad = fabs((double)a[q] - (double)b[q]);
+                    if (ad > ma) ma = ad;
+                }
+            }
+            nd += d_row;
+            rows += d_row > 0;
+        }
+        free(acc); free(a); free(b);
+    }
+    st[0] = nd; st[1] = mu; st[2] = nn; st[3] = rows;
+    *max_abs = ma;
+    l0_free(&s0); l0_free(&s1);
     return 0;
 }
 

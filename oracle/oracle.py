@@ -59,6 +59,9 @@ def lib():
         L.dmo_match.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.dmo_cal_map.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.dmo_set_pow_mode.argtypes = [ctypes.c_int]
+        L.dmo_set_zncc_formula.argtypes = [ctypes.c_int]
+        L.dmo_zncc_formula_diff.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, P, P]
         L.dmo_pow14.argtypes = [ctypes.c_double]
         I, D = ctypes.c_int, ctypes.c_double
         L.dmo_optimize_loop.argtypes = [P, P, I, I, I, I, I, I, D]
@@ -76,6 +79,29 @@ def lib():
 def set_pow_mode(mode):
     """'libm' (numpy-like, default) or 'pinned' (dm_pow.h, what the GPU computes)."""
     lib().dmo_set_pow_mode({'libm': 0, 'pinned': 1}[mode])
+
+
+def set_zncc_formula(name):
+    """'pinned' (default: the kernels' two-multiply formula) or 'f64div'
+    (f32(clamp(num / sqrt(f64 dT * f64 dI)))).  For tools/zncc_pin.py only."""
+    lib().dmo_set_zncc_formula({'pinned': 0, 'f64div': 1}[name])
+
+
+def zncc_formula_diff(img1, img2, ws, feature='cv2.TM_CCOEFF_NORMED'):
+    """Level-0 difference between the two formulas: dict(values, max_ulp, nan_mismatch, rows,
+    max_abs)."""
+    img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    H, W = img1.shape
+    st = np.zeros(4, dtype=np.int64)
+    ma = np.zeros(1, dtype=np.float64)
+    with np.errstate(all='ignore'):
+        rc = lib().dmo_zncc_formula_diff(_p(img1), _p(img2), H, W, ws, METHODS[feature], _p(st), _p(ma))
+    if rc != 0:
+        raise ValueError('dmo_zncc_formula_diff failed: %d' % rc)
+    d = dict(zip(('values', 'max_ulp', 'nan_mismatch', 'rows'), (int(x) for x in st)))
+    d['max_abs'] = float(ma[0])
+    return d
 
 
 def pow14(x):

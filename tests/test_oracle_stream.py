@@ -40,3 +40,23 @@ def test_stream_equals_materialised(pow_mode, h0, w0, ws, feat, flat):
         _same(O.corr_l0_rows(a, b, ws, rows, feat), l0.reshape(P, P)[rows])
     finally:
         O.set_pow_mode('libm')
+
+
+def test_zncc_formula_pin_is_within_float32_rounding():
+    """the kernels' two-multiply ZNCC (pinned) against SURVEY 8(c)'s
+    f64-division formula moves level-0 values by float32 rounding only (|d| <= 2^-21 on
+    [0, 1], no NaN moved) and, on this tile, no integer correspondence
+    (tools/zncc_pin.py measures 8 C3 tiles: profiles/zncc_pin.json)."""
+    a, b = stereo_pair(36, 36, seed=0, dx=2, max_disp=8, sinusoidal=True)
+    d = O.zncc_formula_diff(a, b, 5)
+    assert d['nan_mismatch'] == 0 and d['values'] > 0
+    assert d['max_abs'] <= 2.0 ** -21
+    res = {}
+    for f in ('pinned', 'f64div'):
+        O.set_zncc_formula(f)
+        try:
+            lev, _, _ = O.pyramid_stream(a, b, 5)
+            res[f] = O.match_stream(a, b, 5, lev, sub_pix=False)
+        finally:
+            O.set_zncc_formula('pinned')
+    assert np.array_equal(res['pinned'][:2], res['f64div'][:2])
