@@ -133,7 +133,7 @@ def volume_roofline(solver, reps=3, f16=False):
     gbs = esz * voxels / (ms * 1e-3) / 1e9
     del vol, pyr
     torch.cuda.empty_cache()
-    name = 'dm_corr_volume_f16 (k_volume_cs, binary16)' if f16 else 'dm_corr_volume (k_volume_cs)'
+    name = 'dm_corr_volume_f16 (k_volume_ls, binary16)' if f16 else 'dm_corr_volume (k_volume_ls)'
     return {'kernel': name, 'tiles': batch.T, 'tile': batch.h0,
             'ms': round(ms, 3), 'gvox_s': round(voxels / (ms * 1e-3) / 1e9, 1),
             'algorithmic_bytes_per_voxel': esz, 'bound': 'hbm',

@@ -929,6 +929,23 @@ static int mfq_nw(const dm_tiles *b)
     return b->w0 / 16 / 2 < cap ? b->w0 / 16 / 2 : cap;
 }
 
+// second window region: the column-group layout of k_volume_ls (GW = 16 B of output per
+// lane), prepped by dm_corr_volume(_f16) itself
+static bool volume_ls_shape(const dm_tiles *b)   // sizes the workspace: no environment knobs
+{
+    return mf16_eligible(b) && b->ws <= 5 && (b->h0 % 4) == 0 && ((size_t)(b->h0 / 4) * (b->w0 / 4)) % 8 == 0;
+}
+
+static bool volume_ls_eligible(const dm_tiles *b) { return volume_ls_shape(b) && !mfma_bf16(b); }
+
+static void mfma_views2(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
+{
+    const int G = b->w0 / 16;
+    char *base = (char *)d_stats + align256(base_stats_bytes(b)) + align256(mf16_extra_bytes(b));
+    *Bw = (dm_v4i *)base;
+    *QS = (int2 *)(base + (size_t)b->T * b->h0 * G * 1024);
+}
+
 static void mfma_views(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
 {
     const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
@@ -1093,6 +1110,37 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
     return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st);
 }
 
+// LDS-shared-window volume kernel (k_volume_ls) for the column-group layout (GW == 2, KS == 1,
+// i8 operands); DM_VOLUME_IMPL=cs selects the column-split kernel (A/B), DM_VOLUME_LSNW=8
+// eight waves (patch blocks) per workgroup, DM_VOLUME_NT=0 plain stores.
+template <typename OT>
+static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st)
+{
+    const char *impl = getenv("DM_VOLUME_IMPL");
+    if ((impl && impl[0] == 'c') || !volume_ls_eligible(b)) return DM_ERR_UNSUPPORTED;
+    const int G = b->w0 / 16;
+    const char *nwe = getenv("DM_VOLUME_LSNW"), *nte = getenv("DM_VOLUME_NT");
+    const int nw = (nwe && nwe[0] == '4') ? 4 : 8;
+    const bool nt = !(nte && nte[0] == '0');
+    const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
+    if (bpt % nw) return DM_ERR_UNSUPPORTED;
+    // the window operands in k_volume_ls's layout, in the second window region
+    dm_v4i *Bw;
+    int2 *QS;
+    mfma_views2(b, d_stats, &Bw, &QS);
+    const size_t n = (size_t)b->T * b->h0 * G * 16;
+    const int GW = (int)(16 / sizeof(OT)) < G ? (int)(16 / sizeof(OT)) : G;   // = k_volume_ls's GW
+    k_prep_windows16<<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
+    HIP_TRY(hipGetLastError());
+    const unsigned grid = (unsigned)(b->T * bpt / nw);
+    const Geo gg = make_geo(b);
+#define DM_VL(G_, NW_, NT_) if (G == G_ && nw == NW_ && nt == NT_) { k_volume_ls<G_, NW_, NT_, OT><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, out); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_VL(2, 8, true) DM_VL(4, 8, true) DM_VL(8, 8, true) DM_VL(16, 8, true)
+    DM_VL(8, 4, true) DM_VL(16, 4, true) DM_VL(8, 8, false) DM_VL(16, 8, false)
+#undef DM_VL
+    return DM_ERR_UNSUPPORTED;
+}
+
 extern "C" {
 
 int dm_abi_version(void) { return 103; }
@@ -1105,6 +1153,7 @@ size_t dm_stats_bytes(const dm_tiles *b)
     size_t n = base_stats_bytes(b), extra = 0;
     if (b->ws >= 1 && b->ws <= 15 && b->T > 0 && b->h0 > 0 && b->w0 > 0 && mf16_eligible(b))
         extra = mf16_extra_bytes(b);
+    if (extra && volume_ls_shape(b)) return align256(n) + align256(extra) + extra;  // + the GW = G region
     return extra ? align256(n) + extra : n;
 }
 
@@ -1209,6 +1258,7 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
+        if (launch_volume_ls<float>(b, d_stats, s, d_l0, (hipStream_t)stream) == DM_OK) return DM_OK;
         const char *cs = getenv("DM_VOLUME_CS");
         const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
         const bool bf = mfma_bf16(b);
@@ -1282,6 +1332,7 @@ int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *s
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
+        if (launch_volume_ls<_Float16>(b, d_stats, s, out, st) == DM_OK) return DM_OK;
         const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
         if (b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
             // the float32 column-split kernel with a binary16 stage: 4 rows per store burst

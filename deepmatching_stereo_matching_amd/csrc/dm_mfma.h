@@ -1044,6 +1044,191 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
     }
 }
 
+// ===================================================================================
+// Level-0 volume with LDS-shared windows (k_volume_ls).
+// The column-split kernels above are bound by the per-CU vector-memory pipe, not by the
+// VALU: PMC TA_TA_BUSY / TD_TD_BUSY 0.98 of the cycles (profiles/r02_pmc_mem.txt), because
+// every wave streams its own copy of the window fragments (1 KB of B + 512 B of window
+// stats per 16x16 tile).  Here the NW waves of a workgroup hold DIFFERENT patches (16 each,
+// a 2x2 block of level-1 cells) and sweep ALL windows of the tile; each image row's G
+// window tiles and their stats are staged in LDS once per workgroup by LDS-DMA
+// (buffer_load_dwordx4 ... lds), double-buffered with one barrier per row -- 1/NW of the
+// load traffic per voxel.  A wave owns its patches over every window, so the per-patch
+// min/max needs no cross-wave step.  The windows are laid out in column groups of GW = 16 B
+// of output per lane (8 tiles binary16, 4 float32; dm_corr_volume preps this layout into a
+// second region): lane c of tile tau is window q1 = 16 GW (tau / GW) + GW c + tau % GW, so
+// after a group a lane holds GW consecutive windows of each of its 4 patches and writes them
+// with one 16-B store straight from registers: 16 lanes = one contiguous 256-B patch-row
+// run per store instruction, no LDS stage.
+// Arithmetic per voxel is k_volume_cs's (same y, r, Markstein x): bit-identical output.
+// ===================================================================================
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS byte address m0 + 16 * lane;
+// m0 is saved and restored around it (the compiler owns m0)
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff, unsigned soff)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
+template <int G, int NW, bool NT, typename OT, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
+__global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+                                                   const int2 *__restrict__ QS, OT *vol)
+{
+    constexpr int W0 = 16 * G;
+    constexpr int QB = G * 128;            // bytes of one row's window stats (16 x int2 per tile)
+    constexpr int NQ = (QB + 1023) / 1024; // LDS-DMA instructions for them (1 KB each)
+    constexpr int BUF = (G + NQ) * 1024;   // one row: G B tiles, then the stats
+    constexpr int NL = G + NQ;             // LDS-DMA instructions per row per workgroup
+    static_assert(G % 2 == 0, "tiles come in column-group pairs");
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF]; // the only LDS object (glds rule)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, grp = lane >> 4;
+    const int h0 = g.h0, n = g.ws * g.ws, P = h0 * W0;
+    const int nbj = W0 / 4, bpt = (h0 / 4) * nbj;  // 16-patch blocks per tile (bpt % NW == 0)
+    const int blk = blockIdx.x * NW + wave;
+    const int t = blk / bpt;                       // the same tile for every wave of the block
+    const int I0 = 2 * ((blk % bpt) / nbj), J0 = 2 * ((blk % bpt) % nbj);
+    const size_t tb = (size_t)t * P;
+
+    dm_v4i A[1];
+    build_a<1, false>(A, g, t, I0, J0, c, grp);
+    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
+    int sTr[4];
+    float sTf[4], ap[4];
+    OT *out[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+        sTr[r] = s.sT[tb + p];
+        sTf[r] = (float)sTr[r];
+        ap[r] = s.aP[tb + p];
+        out[r] = vol + (tb + p) * (size_t)P + GW * c;
+    }
+    const dm_v4i acc0 = {DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS};
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(Bw + (size_t)t * h0 * G * 64), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rQ =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(QS + (size_t)t * h0 * G * 16), 0, 0x7fffffff, 0x00020000);
+
+    // LDS-DMA of row q0 into buffer `buf`: instruction i of the row goes to wave i % NW.
+    // Issued through inline asm so that the compiler's wait insertion does not treat every
+    // later ds_read as dependent on it (it would wait vmcnt(0) -- the prefetch AND the
+    // stores -- before the first read of each row); the waits are the explicit vmcnt(N)
+    // before each row's barrier.
+    const unsigned lds0 = (unsigned)(uintptr_t)&lds[0];
+    auto fill = [&](int q0, int buf) {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            if (i % NW != wave) continue;
+            const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)(buf * BUF + i * 1024));
+            if (i < G) {
+                lds_dma16(rB, dst, (unsigned)lane * 16u, (unsigned)(q0 * G + i) * 1024u);
+            } else {
+                const unsigned off = (unsigned)(i - G) * 1024u + (unsigned)lane * 16u;
+                if (off < (unsigned)QB) lds_dma16(rQ, dst, off, (unsigned)(q0 * QB));
+            }
+        }
+    };
+    // tile tau of the row in buffer buf: MFMA + y of this lane's 4 patches
+    auto tile_y = [&](int buf, int tau, float *y) {
+        const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
+        const int2 qs = *(const int2 *)&lds[buf * BUF + G * 1024 + tau * 128 + c * 8];
+        dm_v4i bfr[1] = {bf};
+        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs, n, y);
+    };
+
+    fill(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+
+    // ---- sweep 1: min / max of y over every window (this wave's patches only) ----
+    float mn[4], mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
+    for (int q0 = 0; q0 < h0; ++q0) {
+        const int buf = q0 & 1;
+        fill(q0 + 1 < h0 ? q0 + 1 : 0, buf ^ 1);     // the last prefetch is sweep 2's row 0
+#pragma unroll
+        for (int tau = 0; tau < G; tau += 2) {
+            float y0[4], y1[4];
+            tile_y(buf, tau, y0);
+            tile_y(buf, tau + 1, y1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                mn[r] = fminf(mn[r], fminf(y0[r], y1[r]));
+                mx[r] = fmaxf(mx[r], fmaxf(y0[r], y1[r]));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    float lo[4], hi[4], rmn[4], den[4], rinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        for (int off = 1; off < 16; off <<= 1) {
+            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
+            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        rmn[r] = r_of_y(mn[r], ap[r], g.method);
+        const float rmx = r_of_y(mx[r], ap[r], g.method);
+        den[r] = __fsub_rn(rmx, rmn[r]);
+        rinv[r] = __frcp_rn(den[r]);
+        const bool cc = g.method == DM_TM_CCOEFF;
+        lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
+        hi[r] = cc ? INFINITY : 1.0f;
+        if (c == 0) {
+            const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+            s.rmn[tb + p] = rmn[r];
+            s.rmx[tb + p] = rmx;
+        }
+    }
+
+    // ---- sweep 2: x of every window; lane c holds windows G c .. G c + G - 1 of each of its
+    // 4 patches, stored in 16-B pieces (CH tiles) straight from registers ----
+    constexpr int CH = GW;                 // tiles per column group = per store (16 B or the row)
+    constexpr int STORES = 4 * (G / CH);   // store instructions per row per wave
+    typedef OT ov __attribute__((ext_vector_type(CH)));
+    for (int q0 = 0; q0 < h0; ++q0) {
+        const int buf = (h0 + q0) & 1;
+        if (q0 + 1 < h0) fill(q0 + 1, buf ^ 1);
+#pragma unroll
+        for (int t0 = 0; t0 < G; t0 += CH) {
+            ov v[4];
+#pragma unroll
+            for (int tw = 0; tw < CH; ++tw) {
+                float y[4];
+                tile_y(buf, t0 + tw, y);
+                const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
+                const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
+                const float rr[4] = {__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1]),
+                                     __builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
+                const dm_f2 a01 = dm_f2{rr[0], rr[1]} - dm_f2{rmn[0], rmn[1]};
+                const dm_f2 a23 = dm_f2{rr[2], rr[3]} - dm_f2{rmn[2], rmn[3]};
+                const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
+                const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
+                const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
+                const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
+                const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
+                const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
+                v[0][tw] = (OT)x01.x; v[1][tw] = (OT)x01.y; v[2][tw] = (OT)x23.x; v[3][tw] = (OT)x23.y;
+            }
+            const int col = q0 * W0 + 16 * t0;    // column group t0 / GW starts at window 16 GW (t0 / GW)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (NT) __builtin_nontemporal_store(v[r], (ov *)(out[r] + col));
+                else *(ov *)(out[r] + col) = v[r];
+            }
+        }
+        // this row's prefetch has landed once at most the row's own stores are outstanding
+        if (q0 + 1 < h0) {
+            if constexpr (STORES == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+            else if constexpr (STORES == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+            else if constexpr (STORES == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+}
+
 static bool mf16_eligible(const dm_tiles *b)
 {
     // w0 in {32, 64, 128, 256}: the instantiated column-group counts G = w0/16 = 2, 4, 8, 16

@@ -16,7 +16,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PASSES = {'l12': ('k_level1_mfq', None, 'level1'), 'v16': ('k_volume_cs', True, 'volume_f16')}
+PASSES = {'l12': ('k_level1_mfq', None, 'level1'), 'v16': ('k_volume_ls', True, 'volume_f16')}
 
 
 def _is(name, prefix):

@@ -16,7 +16,8 @@ from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
 from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
-KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS', 'DM_VOLUME_MINW')
+KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS', 'DM_VOLUME_MINW', 'DM_VOLUME_IMPL',
+         'DM_VOLUME_LSNW')
 
 
 def main():
