@@ -55,7 +55,8 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
     float bq;
     if (g.method == DM_TM_CCOEFF) bq = 1.0f;
     else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
-    QS[idx] = make_int2(__float_as_int((float)-s), __float_as_int(bq)); // exact: |s| <= 225*128
+    const int qx = __float_as_int((float)-s), qy = __float_as_int(bq); // exact: |s| <= 225*128
+    QS[idx] = make_int2(qx, qy);
     const size_t tile = idx / 16; // (t, q0, tau)
     if (bf) { // bf16 operands (v_mfma_f32_16x16x32_bf16, K = 32 >= n): lane c+16hq, taps 8hq..8hq+7
         for (int hq = 0; hq < 4; ++hq) {
@@ -80,10 +81,26 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
                 if (k < n) val = (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128;
                 w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
             }
+            if (KS == 1 && n <= 32 && hq >= 2) { // taps 32..63 are zero in every A row: these
+                w[0] = w[2] = qx;                // lanes carry the window's stats instead
+                w[1] = w[3] = qy;                // (qs_of_frag: one 16-B load per lane per tile)
+            }
             dm_v4i o;
             o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
             Bw[(tile * KS + ks) * 64 + c + 16 * hq] = o;
         }
+}
+
+// Window stats of this lane's window from its own B fragment (KS == 1, n <= 32, i8): lanes
+// 32..63 (taps 32..63, multiplied by A's zero padding) hold {qx, qy, qx, qy} = {f32 bits of
+// -sum(I'), b_q} of window c twice.  v_permlane32_swap(vdst = b.z, vsrc = b.x) leaves vsrc =
+// {b.z rows 2, 3 ; b.x rows 2, 3} = qx in every row (same for b.w / b.y); two different
+// registers, so no copy -- the fragment is dead after its MFMA.
+__device__ __forceinline__ int2 qs_of_frag(const dm_v4i &b)
+{
+    const auto x = __builtin_amdgcn_permlane32_swap((unsigned)b.z, (unsigned)b.x, false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap((unsigned)b.w, (unsigned)b.y, false, false);
+    return make_int2((int)x[1], (int)y[1]);
 }
 
 template <int KS>
@@ -405,11 +422,21 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
 // ===================================================================================
 __device__ __forceinline__ double nanmax_d(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
 
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS byte address m0 + 16 * lane;
+// m0 is saved and restored around it (the compiler owns m0)
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff, unsigned soff)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
 // L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
 template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
+    constexpr bool EQ = KS == 1 && YF && !BF;    // window stats ride in the B tile (qs_of_frag)
     __shared__ PowLds plds;
     // [pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at q1 = 16*GW*(w+1)-1,
     // slot 0 = -inf (no window left of column 0)
@@ -474,8 +501,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
                 f.b[tw][ks] = __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (ti * KS + ks) * 1024u, 0);
-            const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
-            f.q[tw] = make_int2(qv.x, qv.y);
+            if constexpr (!EQ) {
+                const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
+                f.q[tw] = make_int2(qv.x, qv.y);
+            }
         }
     };
 
@@ -488,7 +517,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         for (int tw = 0; tw < GW; ++tw) {
             const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 mn[r] = fminf(mn[r], y[r]);
@@ -560,7 +589,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         for (int tw = 0; tw < GW; ++tw) {
             const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : f.q[tw], n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if ((tw & 1) == 0) Cm[tw / 2][r] = tw == 0 ? y[r] : fmaxf(last[r], y[r]);
@@ -1062,24 +1091,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 // run per store instruction, no LDS stage.
 // Arithmetic per voxel is k_volume_cs's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
-// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS byte address m0 + 16 * lane;
-// m0 is saved and restored around it (the compiler owns m0)
-__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff, unsigned soff)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
-}
-
 template <int G, int NW, bool NT, typename OT, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                    const int2 *__restrict__ QS, OT *vol)
 {
     constexpr int W0 = 16 * G;
-    constexpr int QB = G * 128;            // bytes of one row's window stats (16 x int2 per tile)
-    constexpr int NQ = (QB + 1023) / 1024; // LDS-DMA instructions for them (1 KB each)
-    constexpr int BUF = (G + NQ) * 1024;   // one row: G B tiles, then the stats
-    constexpr int NL = G + NQ;             // LDS-DMA instructions per row per workgroup
+    constexpr int BUF = G * 1024;          // one row: G B tiles (window stats inside, qs_of_frag)
+    constexpr int NL = G;                  // LDS-DMA instructions per row per workgroup
     static_assert(G % 2 == 0, "tiles come in column-group pairs");
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF]; // the only LDS object (glds rule)
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1109,8 +1127,6 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
     const dm_v4i acc0 = {DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS};
     const __amdgpu_buffer_rsrc_t rB =
         __builtin_amdgcn_make_buffer_rsrc((void *)(Bw + (size_t)t * h0 * G * 64), 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rQ =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(QS + (size_t)t * h0 * G * 16), 0, 0x7fffffff, 0x00020000);
 
     // LDS-DMA of row q0 into buffer `buf`: instruction i of the row goes to wave i % NW.
     // Issued through inline asm so that the compiler's wait insertion does not treat every
@@ -1123,20 +1139,15 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
         for (int i = 0; i < NL; ++i) {
             if (i % NW != wave) continue;
             const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)(buf * BUF + i * 1024));
-            if (i < G) {
-                lds_dma16(rB, dst, (unsigned)lane * 16u, (unsigned)(q0 * G + i) * 1024u);
-            } else {
-                const unsigned off = (unsigned)(i - G) * 1024u + (unsigned)lane * 16u;
-                if (off < (unsigned)QB) lds_dma16(rQ, dst, off, (unsigned)(q0 * QB));
-            }
+            lds_dma16(rB, dst, (unsigned)lane * 16u, (unsigned)(q0 * G + i) * 1024u);
         }
     };
-    // tile tau of the row in buffer buf: MFMA + y of this lane's 4 patches
+    // tile tau of the row in buffer buf: MFMA + y of this lane's 4 patches (the window stats
+    // ride in the tile's lanes 32..63: qs_of_frag)
     auto tile_y = [&](int buf, int tau, float *y) {
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
-        const int2 qs = *(const int2 *)&lds[buf * BUF + G * 1024 + tau * 128 + c * 8];
         dm_v4i bfr[1] = {bf};
-        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs, n, y);
+        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs_of_frag(bf), n, y);
     };
 
     fill(0, 0);
