@@ -68,7 +68,7 @@ def parse():
 
 class PairSolver:
     """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
-    dominant kernel (dm_corr_level1)."""
+    dominant kernel (dm_corr_level12)."""
 
     def __init__(self, img1, img2, tile, grid, split=False):
         """split: the pair's tiles are sharded over the ranks (rank r solves tiles r::N) and
@@ -224,14 +224,21 @@ def level_roofline(solver, tile, l1_ms):
              else 'dm_corr_level12 (k_level1_mfq, level 2 fused)')
     pmc = load_pmc(tile) if solver.batch.T == 64 else {}
     roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3)}
-    busy, clk = pmc.get('valu_active_cycles_per_launch'), pmc.get('clock_ghz')
-    if busy and clk:
+    busy, cyc = pmc.get('valu_active_cycles_per_launch'), pmc.get('gpu_cycles_per_launch')
+    if busy and cyc:
+        # the launch's cycle count is taken from the PMC pass (the kernel is deterministic); the
+        # live time then gives the clock it ran at in this run, so achieved / peak is the
+        # measured VALU-busy fraction
         achieved = busy / (l1_ms * 1e-3) / 1e9          # G SIMD-cycles/s with the VALU busy
-        peak = 1024 * clk
+        peak = 1024 * cyc / (l1_ms * 1e-3) / 1e9
         roof.update({'achieved': round(achieved, 1), 'peak': round(peak, 1),
                      'unit': 'G VALU-busy SIMD-cycles/s', 'frac': round(achieved / peak, 4),
-                     'valu_busy_source': 'SQ_ACTIVE_INST_VALU x4 per launch (PMC) / live time; '
-                                         'peak 1024 SIMDs x %.3f GHz (GRBM_GUI_ACTIVE/8/t)' % clk})
+                     'valu_busy_source': 'SQ_ACTIVE_INST_VALU x4 (one quad-cycle per wave64 VALU '
+                                         'instruction) per launch over 1024 SIMDs x GRBM_GUI_ACTIVE/8 '
+                                         'cycles per launch, rocprofv3 --pmc (profiles/pmc_level1.json)'})
+        for k in ('ta_busy_frac', 'td_busy_frac'):
+            if k in pmc:
+                roof[k] = pmc[k]
     else:
         roof.update({'achieved': None, 'peak': None, 'unit': 'G VALU-busy SIMD-cycles/s',
                      'frac': None, 'valu_busy_source': 'no PMC pass for this batch shape'})

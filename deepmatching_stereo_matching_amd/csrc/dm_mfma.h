@@ -102,6 +102,8 @@ __device__ __forceinline__ int2 qs_of_frag(const dm_v4i &b)
     const auto y = __builtin_amdgcn_permlane32_swap((unsigned)b.w, (unsigned)b.y, false, false);
     return make_int2((int)x[1], (int)y[1]);
 }
+// (measured: the same through ds_bpermute -- LDS instead of VALU issue -- ran 4 % slower in
+// the fused level kernel, whose pow tables keep the LDS busy; a separate 8-B stats load 2 %)
 
 template <int KS>
 __device__ __forceinline__ void load_frag(dm_v4i *f, const dm_v4i *__restrict__ Bt, int lane)
@@ -1143,11 +1145,12 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
         }
     };
     // tile tau of the row in buffer buf: MFMA + y of this lane's 4 patches (the window stats
-    // ride in the tile's lanes 32..63: qs_of_frag)
+    // ride in the tile's lanes 32..63: read from the stage at lane 32 + c's slot)
     auto tile_y = [&](int buf, int tau, float *y) {
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
+        const int2 qs = *(const int2 *)&lds[buf * BUF + tau * 1024 + (32 + c) * 16];
         dm_v4i bfr[1] = {bf};
-        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs_of_frag(bf), n, y);
+        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs, n, y);
     };
 
     fill(0, 0);
@@ -1166,9 +1169,9 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
             tile_y(buf, tau, y0);
             tile_y(buf, tau + 1, y1);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                mn[r] = fminf(mn[r], fminf(y0[r], y1[r]));
-                mx[r] = fmaxf(mx[r], fmaxf(y0[r], y1[r]));
+            for (int r = 0; r < 4; ++r) {   // v_min3 / v_max3
+                mn[r] = fminf(fminf(mn[r], y0[r]), y1[r]);
+                mx[r] = fmaxf(fmaxf(mx[r], y0[r]), y1[r]);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");

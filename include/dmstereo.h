@@ -73,7 +73,8 @@ typedef struct dm_tiles {
 /* Size in bytes of the per-batch statistics workspace: per-patch / per-window moments and
  * the per-patch min/max of the level-0 map (6 * 4 * T * P), plus, for shapes the MFMA
  * kernels take, the window operands in MFMA fragment order (T * h0 * (w0/16) * (KS*1024
- * + 128), KS = ceil(ws^2 / 64)). */
+ * + 128), KS = ceil(ws^2 / 64)), and for ws <= 5 a second such region in the volume
+ * kernels' column-group layout (dm_corr_volume and dm_corr_volume_f16 fill it themselves). */
 size_t dm_stats_bytes(const dm_tiles *b);
 
 /* Per-patch and per-window moments.
@@ -221,8 +222,10 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 103 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
- * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing). */
+/* ABI version (major * 100 + minor): 104 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+ * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
+ * stats workspace: a second window-operand region for the volume kernels, window stats
+ * carried inside the operand tiles). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

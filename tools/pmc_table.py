@@ -3,6 +3,7 @@ output directory, plus derived per-CU busy fractions (TA/TD busy sums over 256 C
 (GRBM_GUI_ACTIVE / 8 XCDs))."""
 import collections
 import glob
+import json
 import os
 import sys
 
@@ -10,7 +11,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from valu_summary import _rows  # noqa: E402
 
 
-def main(root):
+COMMIT = {'mem_l12': 'level1', 'mem_v16': 'volume_f16'}
+
+
+def main(root, commit=False):
     for d in sorted(glob.glob(os.path.join(root, '*_*'))):
         if not os.path.isdir(d):
             continue
@@ -38,7 +42,19 @@ def main(root):
             if cyc and c in ('TA_TA_BUSY_sum', 'TD_TD_BUSY_sum', 'TA_BUFFER_TOTAL_CYCLES_sum', 'TD_TC_STALL_sum'):
                 extra = '   per-CU busy frac %.3f' % (v / 256.0 / cyc)
             print('    %-32s %16.6g%s' % (c, v, extra))
+        key = COMMIT.get(os.path.basename(d))
+        if commit and key and cyc:
+            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles',
+                                'pmc_%s.json' % key)
+            rec = json.load(open(path)) if os.path.exists(path) else {}
+            rec['ta_busy_frac'] = round(mean['TA_TA_BUSY_sum'] / 256.0 / cyc, 4)
+            rec['td_busy_frac'] = round(mean['TD_TD_BUSY_sum'] / 256.0 / cyc, 4)
+            rec['tcp_accesses_per_launch'] = mean.get('TCP_TOTAL_CACHE_ACCESSES_sum')
+            rec['mem_note'] = ('tools/pmc_mem.sh: TA_TA_BUSY_sum, TD_TD_BUSY_sum over 256 CUs / '
+                               '(GRBM_GUI_ACTIVE / 8); vector-memory pipe occupancy')
+            with open(path, 'w') as fh:
+                json.dump(rec, fh, indent=1)
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    main(sys.argv[1], '--commit' in sys.argv)

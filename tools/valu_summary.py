@@ -60,6 +60,7 @@ def summarize(d, prefix, f16):
     if 'SQ_ACTIVE_INST_VALU' in mean:
         out['valu_active_cycles_per_launch'] = 4.0 * mean['SQ_ACTIVE_INST_VALU']
     if 'GRBM_GUI_ACTIVE' in mean:
+        out['gpu_cycles_per_launch'] = mean['GRBM_GUI_ACTIVE'] / 8.0
         out['clock_ghz'] = round(mean['GRBM_GUI_ACTIVE'] / 8.0 / t / 1e9, 4)
         if 'SQ_ACTIVE_INST_VALU' in mean:
             out['valu_busy_frac'] = round(out['valu_active_cycles_per_launch'] /
@@ -76,7 +77,7 @@ def main(root, commit=False):
         if commit and s:
             path = os.path.join(REPO, 'profiles', 'pmc_%s.json' % key)
             d = json.load(open(path)) if os.path.exists(path) else {}
-            for k in ('valu_active_cycles_per_launch', 'clock_ghz', 'valu_busy_frac',
+            for k in ('valu_active_cycles_per_launch', 'gpu_cycles_per_launch', 'clock_ghz', 'valu_busy_frac',
                       'valu_insts_per_launch', 'kernel_ms_profiled'):
                 if k in s:
                     d[k] = s[k]
