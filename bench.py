@@ -182,7 +182,12 @@ def cpu_baseline(tiles, tile):
     cores = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
     return {'value': round(vox / dt / 1e9, 5), 'unit': 'Gvox/s', 'cores': cores, 'kind': 'port',
             'sample': '%d tiles of S=%d (%.2f G voxels) of the same workload, oracle/dm_oracle.c '
-                      '(OpenMP), %.2f s' % (tiles, tile, vox / 1e9, dt)}
+                      '(OpenMP), %.2f s' % (tiles, tile, vox / 1e9, dt),
+            # the reference's own Python cannot run on the GPU box (OpenCV and absl are absent
+            # from the image); SURVEY.md section 6 timed it in the survey container
+            'reference_python': {'value': 0.021, 'unit': 'Gvox/s', 'cores': 8,
+                                 'sample': 'one S=128 tile, 12.95 s, reference misc/*.py with the '
+                                           'repo cv2 shim, 8-core Xeon (SURVEY.md section 6)'}}
 
 
 def load_pmc(tile, kernel='level1'):
