@@ -17,6 +17,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../include/dmstereo.h"
 #include "dm_pow.h"
 
@@ -1121,6 +1123,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     const int G = b->w0 / 16;
     const char *nwe = getenv("DM_VOLUME_LSNW"), *nte = getenv("DM_VOLUME_NT");
     const int nw = (nwe && nwe[0] == '4') ? 4 : 8;
+    const bool nw4o5 = nwe && nwe[0] == '4' && nwe[1] == '5';   // "45": 4 waves, 5 waves/SIMD budget
     const bool nt = !(nte && nte[0] == '0');
     const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
     if (bpt % nw) return DM_ERR_UNSUPPORTED;
@@ -1134,6 +1137,11 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
+    if (nw4o5 && G == 8 && nt) {
+        k_volume_ls<8, 4, true, OT, 5><<<grid, 256, 0, st>>>(gg, s, Bw, QS, out);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
 #define DM_VL(G_, NW_, NT_) if (G == G_ && nw == NW_ && nt == NT_) { k_volume_ls<G_, NW_, NT_, OT><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, out); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_VL(2, 8, true) DM_VL(4, 8, true) DM_VL(8, 8, true) DM_VL(16, 8, true)
     DM_VL(8, 4, true) DM_VL(16, 4, true) DM_VL(8, 8, false) DM_VL(16, 8, false)

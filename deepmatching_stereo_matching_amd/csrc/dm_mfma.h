@@ -1093,8 +1093,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 // run per store instruction, no LDS stage.
 // Arithmetic per voxel is k_volume_cs's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
-template <int G, int NW, bool NT, typename OT, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
-__global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
+template <int G, int NW, bool NT, typename OT, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
+__global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                    const int2 *__restrict__ QS, OT *vol)
 {
     constexpr int W0 = 16 * G;
@@ -1177,6 +1177,7 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     float lo[4], hi[4], rmn[4], den[4], rinv[4];
+    bool clamp = false;   // does any r = y * a_p of this wave leave [-1, 1]?
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         for (int off = 1; off < 16; off <<= 1) {
@@ -1190,18 +1191,28 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
         const bool cc = g.method == DM_TM_CCOEFF;
         lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
         hi[r] = cc ? INFINITY : 1.0f;
+        // y * a_p is monotone in y (a_p >= 0), so every r of the patch lies in
+        // [mn * a_p, mx * a_p]: the clamp can only act if those bounds leave [-1, 1] (or for a
+        // constant patch, whose r is pinned to 1)
+        clamp = clamp || (!cc && (ap[r] == 0.0f || __fmul_rn(mx[r], ap[r]) > 1.0f ||
+                                  __fmul_rn(mn[r], ap[r]) < -1.0f));
         if (c == 0) {
             const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
             s.rmn[tb + p] = rmn[r];
             s.rmx[tb + p] = rmx;
         }
     }
+    clamp = __builtin_amdgcn_ballot_w64(clamp) != 0;   // wave-uniform
 
     // ---- sweep 2: x of every window; lane c holds windows G c .. G c + G - 1 of each of its
     // 4 patches, stored in 16-B pieces (CH tiles) straight from registers ----
     constexpr int CH = GW;                 // tiles per column group = per store (16 B or the row)
     constexpr int STORES = 4 * (G / CH);   // store instructions per row per wave
     typedef OT ov __attribute__((ext_vector_type(CH)));
+    // the sweep, with or without the clamp (wave-uniform choice; rare: perfect correlations and
+    // constant patches need it)
+    auto sweep2 = [&](auto clamp_tag) {
+    constexpr bool CL = decltype(clamp_tag)::value;
     for (int q0 = 0; q0 < h0; ++q0) {
         const int buf = (h0 + q0) & 1;
         if (q0 + 1 < h0) fill(q0 + 1, buf ^ 1);
@@ -1214,10 +1225,13 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
                 tile_y(buf, t0 + tw, y);
                 const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
                 const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
-                const float rr[4] = {__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1]),
-                                     __builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
-                const dm_f2 a01 = dm_f2{rr[0], rr[1]} - dm_f2{rmn[0], rmn[1]};
-                const dm_f2 a23 = dm_f2{rr[2], rr[3]} - dm_f2{rmn[2], rmn[3]};
+                dm_f2 r01 = ya, r23 = yb;
+                if constexpr (CL) {
+                    r01 = dm_f2{__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1])};
+                    r23 = dm_f2{__builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
+                }
+                const dm_f2 a01 = r01 - dm_f2{rmn[0], rmn[1]};
+                const dm_f2 a23 = r23 - dm_f2{rmn[2], rmn[3]};
                 const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
                 const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
                 const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
@@ -1241,6 +1255,9 @@ __global__ __launch_bounds__(64 * NW) void k_volume_ls(Geo g, Stats s, const dm_
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
     }
+    };
+    if (clamp) sweep2(std::true_type{});
+    else sweep2(std::false_type{});
 }
 
 static bool mf16_eligible(const dm_tiles *b)
