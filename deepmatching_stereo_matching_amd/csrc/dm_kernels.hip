@@ -37,17 +37,26 @@ __device__ __forceinline__ double pow14(double x)
 // Fast-path tables staged in LDS by the level-1 kernels (gathers with random rows: strides
 // of 8 and 16 B spread over the banks; one 32-B row per index conflicted 4x more, measured):
 //   fc[i], fp[i] = c_i, (1/c_i)^y hi, lo                   per mantissa index
-//   gz[k]   = 2^(yE) hi, lo for E = k - 1 + EMIN (k >= 1);  gz[0] = 0 (x == 0 -> +0)
-//   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127), else 0
+//   gz[k]   = 2^(yE) hi, lo for E = k - 1 + EMIN (1 <= k < DM_GZ_ROWS);  gz[0] = 0 (x == 0
+//             -> +0);  gz[DM_GZ_ROWS] = NaN (pow14_q4's row for a NaN input)
+//   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127); g32[255] = NaN
+//             (x = NaN -> NaN); else 0
 // Same constants and the same operation sequence as dm_pow14_fast, so every variant below
 // returns dm_pow14's value on its domain.
 #define DM_GZ_ROWS (2 - DM_POWF_EMIN)
 typedef double dm_d2 __attribute__((ext_vector_type(2)));
 // 16-B rows as one vector: ds_read_b128 (4 LDS cycles, 64 banks) instead of ds_read2_b64
 // (8 cycles, 32 banks) -- MI355X_MICROARCH.md section LDS
+#ifndef DM_POW_SPLIT
+#define DM_POW_SPLIT 0
+#endif
 struct PowLds {
+#if DM_POW_SPLIT
+    double fph[DM_POWF_NT], fpl[DM_POWF_NT]; // (1/c_i)^y hi, lo: same i*8 address as fc
+#else
     dm_d2 fp[DM_POWF_NT];
-    dm_d2 gz[DM_GZ_ROWS];
+#endif
+    dm_d2 gz[DM_GZ_ROWS + 1];
     dm_d2 g32[256];
     double fc[DM_POWF_NT];
 };
@@ -56,15 +65,22 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
 {
     for (int i = tid; i < DM_POWF_NT; i += nthreads) {
         t.fc[i] = c_powf_c[i];
+#if DM_POW_SPLIT
+        t.fph[i] = c_powf_p[2 * i];
+        t.fpl[i] = c_powf_p[2 * i + 1];
+#else
         t.fp[i] = dm_d2{c_powf_p[2 * i], c_powf_p[2 * i + 1]};
+#endif
     }
-    for (int k = tid; k < DM_GZ_ROWS; k += nthreads) {
-        t.gz[k] = k ? dm_d2{c_powf_g[2 * (k - 1)], c_powf_g[2 * (k - 1) + 1]} : dm_d2{0.0, 0.0};
+    for (int k = tid; k <= DM_GZ_ROWS; k += nthreads) {
+        t.gz[k] = k == DM_GZ_ROWS ? dm_d2{(double)NAN, (double)NAN}
+                  : k ? dm_d2{c_powf_g[2 * (k - 1)], c_powf_g[2 * (k - 1) + 1]} : dm_d2{0.0, 0.0};
     }
     for (int b = tid; b < 256; b += nthreads) {
         const int e = b - 127 - DM_POWF_EMIN; // row of c_powf_g
         const bool in = b >= 1 && b <= 127 && e >= 0;
-        t.g32[b] = in ? dm_d2{c_powf_g[2 * e], c_powf_g[2 * e + 1]} : dm_d2{0.0, 0.0};
+        t.g32[b] = in ? dm_d2{c_powf_g[2 * e], c_powf_g[2 * e + 1]}
+                   : b == 255 ? dm_d2{(double)NAN, (double)NAN} : dm_d2{0.0, 0.0};
     }
 }
 
@@ -78,8 +94,12 @@ __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const Pow
     q = fma(q, r, DM_POWF_B2);
     q = fma(q, r, DM_POWF_B1);
     q = q * r;
+#if DM_POW_SPLIT
+    const double Phi = t.fph[i], Plo = t.fpl[i];
+#else
     const dm_d2 Pr = t.fp[i];
     const double Phi = Pr.x, Plo = Pr.y;
+#endif
     const double Blo = fma(Phi, q, Plo);
     const double Ghi = G.x, Glo = G.y;
     const double Zhi = Phi * Ghi;
@@ -102,10 +122,24 @@ __device__ __forceinline__ double pow14_zd(double x, const PowLds &t)
     return pow14_core(M, i, t.gz[k], t);
 }
 
+// pow14(s / 4) for s == 0, NaN, or s / 4 in [2^EMIN, 1]: /4 of a normal double only lowers
+// its biased exponent by 2 (same mantissa, same table index), so the scaling is folded into
+// the row index -- no multiply.  NaN reads the NaN row and returns NaN.
+__device__ __forceinline__ double pow14_q4(double s, const PowLds &t)
+{
+    const uint64_t b = dm_bits_f64(s);
+    const unsigned hi = (unsigned)(b >> 32);
+    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int i = (int)((hi >> 11) & (DM_POWF_NT - 1));
+    const int be = (int)((hi >> 20) & 0x7FF);
+    const int k = min(max(be - (1024 + DM_POWF_EMIN), 0), DM_GZ_ROWS);
+    return pow14_core(M, i, t.gz[k], t);
+}
+
 // float32 input (widened exactly): exact dm_pow14((double)x) for x == 0 and for normal
-// x in [2^EMIN, 1] (f32 subnormals would need renormalising: callers never produce them).
-// NaN gives garbage (callers add a NaN term).  Fewer integer ops than pow14_zd: exponent,
-// index and mantissa come straight from the f32 bits.
+// x in [2^EMIN, 1] (f32 subnormals would need renormalising: callers never produce them);
+// NaN -> NaN (the g32 NaN row).  Fewer integer ops than pow14_zd: exponent, index and
+// mantissa come straight from the f32 bits.
 __device__ __forceinline__ double pow14_zf(float x, const PowLds &t)
 {
     const unsigned u = __float_as_uint(x);

@@ -82,8 +82,8 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
                 w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
             }
             if (KS == 1 && n <= 32 && hq >= 2) { // taps 32..63 are zero in every A row: these
-                w[0] = w[2] = qx;                // lanes carry the window's stats instead
-                w[1] = w[3] = qy;                // (qs_of_frag: one 16-B load per lane per tile)
+                w[0] = w[3] = qx;                // lanes carry the window's stats instead
+                w[1] = w[2] = qy;                // (qs_of_frag: one 16-B load per lane per tile)
             }
             dm_v4i o;
             o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
@@ -92,16 +92,20 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
 }
 
 // Window stats of this lane's window from its own B fragment (KS == 1, n <= 32, i8): lanes
-// 32..63 (taps 32..63, multiplied by A's zero padding) hold {qx, qy, qx, qy} = {f32 bits of
-// -sum(I'), b_q} of window c twice.  v_permlane32_swap(vdst = b.z, vsrc = b.x) leaves vsrc =
-// {b.z rows 2, 3 ; b.x rows 2, 3} = qx in every row (same for b.w / b.y); two different
-// registers, so no copy -- the fragment is dead after its MFMA.
-__device__ __forceinline__ int2 qs_of_frag(const dm_v4i &b)
+// 32..63 (taps 32..63, multiplied by A's zero padding) hold {qx, qy, qy, qx}, qx = f32 bits
+// of -sum(I'), qy = b_q of window c.  v_permlane32_swap(vdst = b.w, vsrc = b.x) leaves vsrc =
+// {b.w rows 2, 3 ; b.x rows 2, 3} = qx in every row (same for b.y / b.z -> qy).  The results
+// sit in b.x and b.z, the LOW halves of register pairs, which the packed y arithmetic
+// broadcasts with op_sel_hi = 0 in place -- no copies; the fragment is dead after its MFMA.
+// (k_volume_ls reads {qx, qy} as one aligned 8-B pair at the row's start instead.)
+typedef float dm_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dm_f2 qs_of_frag(const dm_v4i &b)
 {
-    const auto x = __builtin_amdgcn_permlane32_swap((unsigned)b.z, (unsigned)b.x, false, false);
-    const auto y = __builtin_amdgcn_permlane32_swap((unsigned)b.w, (unsigned)b.y, false, false);
-    return make_int2((int)x[1], (int)y[1]);
+    const auto x = __builtin_amdgcn_permlane32_swap((unsigned)b.w, (unsigned)b.x, false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap((unsigned)b.y, (unsigned)b.z, false, false);
+    return dm_f2{__uint_as_float(x[1]), __uint_as_float(y[1])};
 }
+__device__ __forceinline__ dm_f2 qs_pair(int2 q) { return dm_f2{__int_as_float(q.x), __int_as_float(q.y)}; }
 // (measured: the same through ds_bpermute -- LDS instead of VALU issue -- ran 4 % slower in
 // the fused level kernel, whose pow tables keep the LDS busy; a separate 8-B stats load 2 %)
 
@@ -144,28 +148,28 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
 // (sTf = f32(sum T'), qs.x = f32 bits of -sum(I')) -- the integer path's f32(num) in 1.5
 // packed instructions per voxel instead of 2.
 #define DM_YBIAS 0x4B400000
-typedef float dm_f2 __attribute__((ext_vector_type(2)));
 
 template <bool YF, bool BF = false>
-__device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, const float *sTf, int2 qs, int n,
+__device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, const float *sTf, dm_f2 q2, int n,
                                          float *y)
 {
-    const float b = __int_as_float(qs.y);
     if constexpr (YF) {
-        const float nf = (float)n, sI = __int_as_float(qs.x);
+        const float nf = (float)n;
         const float nb = BF ? 0.0f : -nf * 12582912.0f;   // exact (see above)
+        const dm_f2 sI2 = __builtin_shufflevector(q2, q2, 0, 0), b2 = __builtin_shufflevector(q2, q2, 1, 1);
         const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
         const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
         const dm_f2 m01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, dm_f2{nb, nb});
         const dm_f2 m23 = __builtin_elementwise_fma(a23, dm_f2{nf, nf}, dm_f2{nb, nb});
-        const dm_f2 n01 = __builtin_elementwise_fma(dm_f2{sTf[0], sTf[1]}, dm_f2{sI, sI}, m01);
-        const dm_f2 n23 = __builtin_elementwise_fma(dm_f2{sTf[2], sTf[3]}, dm_f2{sI, sI}, m23);
-        const dm_f2 y01 = n01 * dm_f2{b, b}, y23 = n23 * dm_f2{b, b};
+        const dm_f2 n01 = __builtin_elementwise_fma(dm_f2{sTf[0], sTf[1]}, sI2, m01);
+        const dm_f2 n23 = __builtin_elementwise_fma(dm_f2{sTf[2], sTf[3]}, sI2, m23);
+        const dm_f2 y01 = n01 * b2, y23 = n23 * b2;
         y[0] = y01.x; y[1] = y01.y; y[2] = y23.x; y[3] = y23.y;
     } else {
+        const float b = q2.y;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
+            y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)q2.x)), b);
     }
 }
 
@@ -451,7 +455,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     constexpr bool LATE = L2F;
     constexpr int L2V = 4 * GW, L2B = 64 / L2V; // level-2 values per wave per row; rows per stash
     __shared__ double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: pow inputs
-    __shared__ double cnan[4];         // [cell]: NaN if a child's map is constant (den == 0), else 0
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
     if (tid < 64) (&xch[0][0][0][0][0])[(tid >> 4) * (NW + 1) * 16 + (tid & 15)] = -INFINITY;
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         for (int tw = 0; tw < GW; ++tw) {
             const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 mn[r] = fminf(mn[r], y[r]);
@@ -567,10 +570,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         f[5 * 4 + r] = __frcp_rn(den);
         s.rmn[tb + p] = rmn;
         s.rmx[tb + p] = rmx;
-        const bool flat = den == 0.0f;
-        const bool any = __shfl(flat, lane - c) || __shfl(flat, lane - c + 1) || __shfl(flat, lane - c + 2) ||
-                         __shfl(flat, lane - c + 3);
-        if (r == 0) cnan[grp] = any ? (double)NAN : 0.0;
     }
     __syncthreads();
 
@@ -591,7 +590,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         for (int tw = 0; tw < GW; ++tw) {
             const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : f.q[tw], n, y);
+            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if ((tw & 1) == 0) Cm[tw / 2][r] = tw == 0 ? y[r] : fmaxf(last[r], y[r]);
@@ -678,11 +677,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 #pragma unroll
         for (int m = 0; m < M; ++m) l1q[m] = l1p[m];
         // row pooling: even row q0 opens level-1 row u, odd row q0 + 1 closes it
-        // a constant child map (den == 0) makes its values NaN (0/0): its pow14_zf is garbage,
-        // the cell's NaN term restores the reference's NaN in the sum and in level 1
+        // a constant child map (den == 0) makes its values NaN (0 * inf in the Markstein step,
+        // the reference's 0/0): pow14_zf and pow14_q4 map NaN to NaN, so the sum and level 1
+        // of its cell are NaN, as in the reference
         const float4 kap = cst[grp][0], klo = cst[grp][1], khi = cst[grp][2], kmn = cst[grp][3],
                      kden = cst[grp][4], kinv = cst[grp][5];
-        const double nanc = cnan[grp];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             float R[4], x[4];
@@ -709,8 +708,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 const double pv = pow14_zf(x[r], plds);
                 sum = r == 0 ? pv : sum + pv;
             }
-            sum = sum + nanc;
-            l1p[m] = pow14_zd(sum / 4.0, plds) + nanc;
+            l1p[m] = pow14_q4(sum, plds); // pow14(sum / 4)
             if (L1) Lrow[(size_t)u * w1 + M * c + m] = l1p[m];
         }
         if constexpr (L2F) {
@@ -802,7 +800,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, qs_pair(fa.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -810,7 +808,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, qs_pair(fb.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -844,7 +842,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, qs_pair(f.q[tw]), n, y);
             // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
             const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
             const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
@@ -976,7 +974,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, fa.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, qs_pair(fa.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -984,7 +982,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, fb.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, qs_pair(fb.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -1026,7 +1024,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, f.q[tw], n, y);
+            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, qs_pair(f.q[tw]), n, y);
             // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
             const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
             const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
@@ -1148,9 +1146,9 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
     // ride in the tile's lanes 32..63: read from the stage at lane 32 + c's slot)
     auto tile_y = [&](int buf, int tau, float *y) {
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
-        const int2 qs = *(const int2 *)&lds[buf * BUF + tau * 1024 + (32 + c) * 16];
+        const dm_f2 q2 = *(const dm_f2 *)&lds[buf * BUF + tau * 1024 + (32 + c) * 16]; // {qx, qy}
         dm_v4i bfr[1] = {bf};
-        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, qs, n, y);
+        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, q2, n, y);
     };
 
     fill(0, 0);
