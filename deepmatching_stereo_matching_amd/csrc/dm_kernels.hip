@@ -507,11 +507,15 @@ __global__ void k_aggregate(const double *in, int T, int h, int w, int rectify, 
 // band's input rows once (MaxPool columns 2v-1..2v+1, rows streamed), so every input byte
 // is read once from HBM, coalesced.  Children are summed in ul, ur, ll, lr order through
 // LDS.  W2 = w/2 columns per child, 4*W2 threads, BR output rows per band.
+// VEC (16-B aligned input, W2 in {16, 32, 64}: a child's lanes never straddle a wave): one
+// 16-B load of columns 2v, 2v+1 per lane and row; column 2v-1 is lane v-1's second value.
 #define AGG_LDS_DOUBLES 4096
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_aggregate_rows(const double *in, int T, int h, int w, int BR, int rectify,
                                                         double *out)
 {
-    __shared__ double pooled[AGG_LDS_DOUBLES]; // [child][band row][v]
+    extern __shared__ double pooled[]; // [child][band row][v]: 4 * BR * W2 doubles (dynamic, so
+                                       // small bands do not cap the workgroups per CU)
     const int h2 = h / 2, W2 = w / 2;
     const size_t P = (size_t)h * w, P2 = (size_t)h2 * W2;
     const int nb = (h2 + BR - 1) / BR;
@@ -531,8 +535,14 @@ __global__ __launch_bounds__(256) void k_aggregate_rows(const double *in, int T,
             for (int k = 0; k < CH; ++k) {
                 const int a = min(ab + k, a1);
                 const double *row = m + (size_t)a * w;
-                const double x1 = row[2 * v], x2 = row[2 * v + 1], x0 = v > 0 ? row[2 * v - 1] : -INFINITY;
-                cmv[k] = nanmax(nanmax(x0, x1), x2);
+                if constexpr (VEC) {
+                    const dm_d2 x = *(const dm_d2 *)(row + 2 * v);
+                    const double l = __shfl(x.y, (int)(threadIdx.x & 63) - 1);
+                    cmv[k] = nanmax(nanmax(v > 0 ? l : -INFINITY, x.x), x.y);
+                } else {
+                    const double x1 = row[2 * v], x2 = row[2 * v + 1], x0 = v > 0 ? row[2 * v - 1] : -INFINITY;
+                    cmv[k] = nanmax(nanmax(x0, x1), x2);
+                }
             }
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
@@ -651,6 +661,127 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, in
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
 }
 
+// Level-0 values of one patch on demand with its taps in registers (WS known at compile
+// time): the same expression as l0_value.
+template <int WS>
+struct PatchL0 {
+    static constexpr int NW4 = WS / 4 > 0 ? WS / 4 : 1, NR4 = WS % 4 > 0 ? WS % 4 : 1;
+    int Tw[WS][NW4]; // taps 4m..4m+3 of row u as packed signed bytes (v_dot4_i32_i8 operand)
+    int Tb[WS][NR4]; // the WS % 4 remaining taps of row u
+    int sT;
+    float ap, rmn, rmx;
+    // tap k = T'[k / WS][k % WS] (k known at compile time after unrolling)
+    __device__ int tap(int k) const
+    {
+        const int u = k / WS, v = k % WS;
+        return v < 4 * (WS / 4) ? ((int)((unsigned)Tw[u][v >> 2] << (24 - 8 * (v & 3)))) >> 24 : Tb[u][v - 4 * (WS / 4)];
+    }
+    __device__ void load(const Geo &g, const Stats &s, int t, int p0, int p1)
+    {
+        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+        const uint8_t *a = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
+        int T8[WS * WS];
+#pragma unroll
+        for (int k = 0; k < WS * WS; ++k) T8[k] = (int)a[(size_t)(k / WS) * g.pitch1 + (k % WS)] - 128;
+#pragma unroll
+        for (int u = 0; u < WS; ++u) {
+#pragma unroll
+            for (int m = 0; m < WS / 4; ++m) {
+                unsigned w = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w |= (unsigned)(T8[u * WS + 4 * m + k] & 0xFF) << (8 * k);
+                Tw[u][m] = (int)w;
+            }
+#pragma unroll
+            for (int k = 0; k < WS % 4; ++k) Tb[u][k] = T8[u * WS + 4 * (WS / 4) + k];
+        }
+        const size_t op = (size_t)t * g.h0 * g.w0 + (size_t)p0 * g.w0 + p1;
+        sT = s.sT[op]; ap = s.aP[op]; rmn = s.rmn[op]; rmx = s.rmx[op];
+    }
+    // Integer dot products sum_k T'_k I'_k of this patch against the NI x NJ windows whose
+    // top-left window is (qa0, qb0).  The (NI+WS-1) x (NJ+WS-1) image region must lie inside
+    // the tile.  Per region row: its aligned dwords (each holds a needed byte, so no load
+    // leaves the page of a valid byte), re-aligned by the row's byte offset (v_alignbyte),
+    // bytes made signed (^ 0x80 = b - 128 as int8), then v_dot4_i32_i8 over four taps at a
+    // time: (NB+3)/4 loads per row instead of one byte load per tap and window.  Exact
+    // integers, so the sums equal the byte-wise ones.
+    // emit(i, acc_row) is called for window row i as soon as its last image row is in, so a
+    // caller that consumes rows at once keeps only WS rows of sums live.
+    template <int NI, int NJ, typename F>
+    __device__ void grid_rows(const Geo &g, int t, int qa0, int qb0, F &&emit) const
+    {
+        int acc[NI][NJ];
+        constexpr int NB = NJ + WS - 1, NE = (NB + 3) / 4, ND = (NB + 6) / 4;
+        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = 0;
+#pragma unroll
+        for (int r = 0; r < NI + WS - 1; ++r) {
+            const uint8_t *rp = g.img2 + (size_t)(ro + qa0 + r) * g.pitch2 + co + qb0;
+            const unsigned off = (unsigned)((uintptr_t)rp & 3u);
+            const unsigned *A = (const unsigned *)(rp - off);
+            unsigned D[ND + 1], E[NE + 1];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) D[d] = (4 * d <= NB - 1 || 4 * d < (int)off + NB) ? A[d] : 0u;
+            D[ND] = 0u;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) E[e] = __builtin_amdgcn_alignbyte(D[e + 1], D[e], off) ^ 0x80808080u;
+            E[NE] = 0u;
+#pragma unroll
+            for (int u = 0; u < WS; ++u) {
+                const int i = r - u;
+                if (i < 0 || i >= NI) continue;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    int a = acc[i][j];
+#pragma unroll
+                    for (int m = 0; m < WS / 4; ++m) {
+                        const int b0 = j + 4 * m;
+                        const unsigned w = (b0 & 3) ? __builtin_amdgcn_alignbyte(E[(b0 >> 2) + 1], E[b0 >> 2], b0 & 3)
+                                                    : E[b0 >> 2];
+                        a = __builtin_amdgcn_sdot4(Tw[u][m], (int)w, a, false);
+                    }
+#pragma unroll
+                    for (int k = 0; k < WS % 4; ++k) {
+                        const int b = j + 4 * (WS / 4) + k;
+                        a += Tb[u][k] * (((int)(E[b >> 2] << (24 - 8 * (b & 3)))) >> 24);
+                    }
+                    acc[i][j] = a;
+                }
+            }
+            if (r - (WS - 1) >= 0 && r - (WS - 1) < NI) emit(r - (WS - 1), acc[r - (WS - 1)]);
+        }
+    }
+    template <int NI, int NJ>
+    __device__ void grid_acc(const Geo &g, int t, int qa0, int qb0, int (&out)[NI][NJ]) const
+    {
+        grid_rows<NI, NJ>(g, t, qa0, qb0, [&](int i, const int (&row)[NJ]) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) out[i][j] = row[j];
+        });
+    }
+    // rectified level 0 from an integer dot sum (the expression of value() below)
+    __device__ double rect(const Geo &g, const Stats &s, int t, int q0, int q1, int acc) const
+    {
+        const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
+        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
+        return pow14((double)norm_x(r, rmn, rmx));
+    }
+    __device__ double value(const Geo &g, const Stats &s, int t, int q0, int q1) const
+    {
+        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
+        const uint8_t *b = g.img2 + (size_t)(ro + q0) * g.pitch2 + co + q1;
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < WS * WS; ++k) acc += tap(k) * ((int)b[(size_t)(k / WS) * g.pitch2 + (k % WS)] - 128);
+        const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
+        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
+        return pow14((double)norm_x(r, rmn, rmx));
+    }
+};
+
 // The _B step onto level 1 when level 1 was never stored (dm_corr_level12 without level 1):
 // four lanes per entry, one per child patch of the level-1 cell.  A lane computes y on the
 // 7x7 level-0 neighbourhood its entry's 3x3 level-1 window pools from, takes the MaxPool on
@@ -677,31 +808,63 @@ __global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, co
     const int pd1 = (int)(long long)(pm[Pp + par] * 2) + (p1 & 1);
     // child patch (level-0 patch coordinates) and its statistics
     const int pp0 = 2 * p0 + (ch >> 1), pp1 = 2 * p1 + (ch & 1);
-    const size_t op = (size_t)t * P + (size_t)pp0 * w0 + pp1;
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-    int T8[n];
-    {
-        const uint8_t *a = g.img1 + (size_t)(ro + pp0) * g.pitch1 + co + pp1;
+    PatchL0<WS> pt;
+    pt.load(g, s, t, pp0, pp1);
+    const int sT = pt.sT;
+    const float ap = pt.ap, rmn = pt.rmn, rmx = pt.rmx;
+    // MaxPool(3,2,1) on y over level-0 rows/cols 2*pd - 3 .. 2*pd + 3 (-inf outside the map):
+    // R[a][b] = max of y[2a..2a+2][2b..2b+2]
+    float R[3][3];
 #pragma unroll
-        for (int k = 0; k < n; ++k) T8[k] = (int)a[(size_t)(k / ws) * g.pitch1 + (k % ws)] - 128;
-    }
-    const int sT = s.sT[op];
-    const float ap = s.aP[op], rmn = s.rmn[op], rmx = s.rmx[op];
-    // y on level-0 rows/cols 2*pd - 3 .. 2*pd + 3 (-inf outside the map)
-    float y[7][7];
+    for (int a = 0; a < 3; ++a)
 #pragma unroll
-    for (int i = 0; i < 7; ++i)
+        for (int b = 0; b < 3; ++b) R[a][b] = -INFINITY;
+    const int qa0 = 2 * pd0 - 3, qb0 = 2 * pd1 - 3;
+    auto pool_row = [&](int i, const float (&yr)[7]) {
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            const int qa = 2 * pd0 - 3 + i, qb = 2 * pd1 - 3 + j;
-            if (qa < 0 || qa >= h0 || qb < 0 || qb >= w0) { y[i][j] = -INFINITY; continue; }
-            const uint8_t *b = g.img2 + (size_t)(ro + qa) * g.pitch2 + co + qb;
-            int acc = 0;
+        for (int a = 0; a < 3; ++a) {
+            if (i < 2 * a || i > 2 * a + 2) continue;
 #pragma unroll
-            for (int k = 0; k < n; ++k) acc += T8[k] * ((int)b[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128);
-            const size_t oq = (size_t)t * P + (size_t)qa * w0 + qb;
-            y[i][j] = y_of_num(n * acc - sT * s.sI[oq], s.bQ[oq]);
+            for (int b = 0; b < 3; ++b) R[a][b] = fmaxf(R[a][b], fmaxf(fmaxf(yr[2 * b], yr[2 * b + 1]), yr[2 * b + 2]));
         }
+    };
+    bool fast = false;
+    if constexpr (WS <= 7) fast = qa0 >= 0 && qa0 + 6 < h0 && qb0 >= 0 && qb0 + 6 < w0;
+    if constexpr (WS <= 7) {
+        if (fast) { // all 49 windows inside: one pass over their (WS+6)^2 image bytes
+            int acc[7][7];
+            pt.template grid_acc<7, 7>(g, t, qa0, qb0, acc);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                float yr[7];
+#pragma unroll
+                for (int j = 0; j < 7; ++j) {
+                    const size_t oq = (size_t)t * P + (size_t)(qa0 + i) * w0 + qb0 + j;
+                    yr[j] = y_of_num(n * acc[i][j] - sT * s.sI[oq], s.bQ[oq]);
+                }
+                pool_row(i, yr);
+            }
+        }
+    }
+    if (!fast) { // map border (rare): byte loads, one window row at a time
+#pragma unroll 1
+        for (int i = 0; i < 7; ++i) {
+            float yr[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const int qa = qa0 + i, qb = qb0 + j;
+                if (qa < 0 || qa >= h0 || qb < 0 || qb >= w0) { yr[j] = -INFINITY; continue; }
+                const uint8_t *b = g.img2 + (size_t)(ro + qa) * g.pitch2 + co + qb;
+                int acc = 0;
+#pragma unroll
+                for (int k = 0; k < n; ++k) acc += pt.tap(k) * ((int)b[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128);
+                const size_t oq = (size_t)t * P + (size_t)qa * w0 + qb;
+                yr[j] = y_of_num(n * acc - sT * s.sI[oq], s.bQ[oq]);
+            }
+            pool_row(i, yr);
+        }
+    }
     double win[9];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -710,14 +873,7 @@ __global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, co
             const int u = pd0 - 1 + a, v = pd1 - 1 + b;
             double pv = 0.0;
             const bool in = u >= 0 && u < h1 && v >= 0 && v < w1;
-            if (in) {
-                float R = -INFINITY;
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) R = fmaxf(R, y[2 * a + i][2 * b + j]);
-                pv = pow14((double)norm_x(r_of_y(R, ap, g.method), rmn, rmx));
-            }
+            if (in) pv = pow14((double)norm_x(r_of_y(R[a][b], ap, g.method), rmn, rmx));
             // children sum in ul, ur, ll, lr order (lanes 4e + 0..3)
             const int base = (threadIdx.x & 63) & ~3;
             const double v0 = __shfl(pv, base), v1 = __shfl(pv, base + 1), v2 = __shfl(pv, base + 2),
@@ -996,35 +1152,6 @@ static inline unsigned nblk(size_t n, unsigned bs)
     return (unsigned)(b > 0x7fffffff ? 0x7fffffff : b);
 }
 
-// Level-0 values of one patch on demand with its taps in registers (WS known at compile
-// time): the same expression as l0_value.
-template <int WS>
-struct PatchL0 {
-    int T8[WS * WS];
-    int sT;
-    float ap, rmn, rmx;
-    __device__ void load(const Geo &g, const Stats &s, int t, int p0, int p1)
-    {
-        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-        const uint8_t *a = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int k = 0; k < WS * WS; ++k) T8[k] = (int)a[(size_t)(k / WS) * g.pitch1 + (k % WS)] - 128;
-        const size_t op = (size_t)t * g.h0 * g.w0 + (size_t)p0 * g.w0 + p1;
-        sT = s.sT[op]; ap = s.aP[op]; rmn = s.rmn[op]; rmx = s.rmx[op];
-    }
-    __device__ double value(const Geo &g, const Stats &s, int t, int q0, int q1) const
-    {
-        const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-        const uint8_t *b = g.img2 + (size_t)(ro + q0) * g.pitch2 + co + q1;
-        int acc = 0;
-#pragma unroll
-        for (int k = 0; k < WS * WS; ++k) acc += T8[k] * ((int)b[(size_t)(k / WS) * g.pitch2 + (k % WS)] - 128);
-        const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
-        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
-        return pow14((double)norm_x(r, rmn, rmx));
-    }
-};
-
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
 template <int WS>
 __global__ __launch_bounds__(256) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
@@ -1042,13 +1169,27 @@ __global__ __launch_bounds__(256) void k_match_step_l0(Geo g, Stats s, int T, co
     PatchL0<WS> pt;
     pt.load(g, s, t, p0, p1);
     double win[9], o[3];
+    bool fast = false;
+    if constexpr (WS <= 7) fast = pd0 >= 1 && pd0 + 1 < hn && pd1 >= 1 && pd1 + 1 < wn;
+    if constexpr (WS <= 7) {
+        if (fast) { // the 3x3 windows in one pass over their (WS+2)^2 image bytes
+            int acc[3][3];
+            pt.template grid_acc<3, 3>(g, t, pd0 - 1, pd1 - 1, acc);
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+            for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const int r = pd0 - 1 + a, c = pd1 - 1 + b;
-            win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0 : pt.value(g, s, t, r, c);
+                for (int b = 0; b < 3; ++b) win[a * 3 + b] = pt.rect(g, s, t, pd0 - 1 + a, pd1 - 1 + b, acc[a][b]);
         }
+    }
+    if (!fast) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const int r = pd0 - 1 + a, c = pd1 - 1 + b;
+                win[a * 3 + b] = (r < 0 || r >= hn || c < 0 || c >= wn) ? 0.0 : pt.value(g, s, t, r, c);
+            }
+    }
     near_pick(win, pd0, pd1, o);
     double *cm_ = cmap + (size_t)t * 3 * Pn;
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
@@ -1069,6 +1210,20 @@ __global__ __launch_bounds__(256) void k_subpix_t(Geo g, Stats s, int T, double 
     pt.load(g, s, t, p0, p1);
     const double row = mt[pc], col = mt[P + pc];
     const int c0 = (int)row, c1 = (int)col;
+    if constexpr (WS <= 7) {
+        if (c0 >= 1 && c0 + 1 < h0 && c1 >= 1 && c1 + 1 < w0) {
+            // interior: the five values (centre, up/down, left/right) from one 3x3 pass, and
+            // neither the IndexError nor the -1 wrap branch applies
+            int acc[3][3];
+            pt.template grid_acc<3, 3>(g, t, c0 - 1, c1 - 1, acc);
+            const double r0 = pt.rect(g, s, t, c0, c1, acc[1][1]);
+            mt[pc] = ((double)p0 - ((double)p0 - row)) +
+                     sub_pix_compute(r0, pt.rect(g, s, t, c0 + 1, c1, acc[2][1]), pt.rect(g, s, t, c0 - 1, c1, acc[0][1]));
+            mt[P + pc] = ((double)p1 - ((double)p1 - col)) +
+                         sub_pix_compute(r0, pt.rect(g, s, t, c0, c1 + 1, acc[1][2]), pt.rect(g, s, t, c0, c1 - 1, acc[1][0]));
+            return;
+        }
+    }
     const double r0 = pt.value(g, s, t, c0, c1);
     const double dx = (double)p0 - row;
     double nrow, ncol;
@@ -1448,7 +1603,10 @@ int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t re
         const int BR = AGG_LDS_DOUBLES / (4 * W2) < h2 ? AGG_LDS_DOUBLES / (4 * W2) : h2;
         const size_t nwg = (size_t)T * h2 * W2 * ((h2 + BR - 1) / BR);
         if (nwg <= 0x7fffffff) {
-            k_aggregate_rows<<<(unsigned)nwg, 4 * W2, 0, (hipStream_t)stream>>>(d_in, T, h, w, BR, rectify, d_out);
+            const bool vec = ((uintptr_t)d_in & 15) == 0 && (W2 == 16 || W2 == 32 || W2 == 64);
+            const size_t lds = (size_t)4 * BR * W2 * sizeof(double);
+            if (vec) k_aggregate_rows<true><<<(unsigned)nwg, 4 * W2, lds, (hipStream_t)stream>>>(d_in, T, h, w, BR, rectify, d_out);
+            else k_aggregate_rows<false><<<(unsigned)nwg, 4 * W2, lds, (hipStream_t)stream>>>(d_in, T, h, w, BR, rectify, d_out);
             HIP_TRY(hipGetLastError());
             return DM_OK;
         }
