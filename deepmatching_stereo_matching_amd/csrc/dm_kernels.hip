@@ -1322,7 +1322,8 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     mfma_views2(b, d_stats, &Bw, &QS);
     const size_t n = (size_t)b->T * b->h0 * G * 16;
     const int GW = (int)(16 / sizeof(OT)) < G ? (int)(16 / sizeof(OT)) : G;   // = k_volume_ls's GW
-    k_prep_windows16<<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
+    if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
+    else k_prep_windows16<0><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
@@ -1371,8 +1372,9 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
         const size_t n = (size_t)b->T * b->h0 * G * 16;
         const int GW = var == 3 ? G / mfq_nw(b) : G;
-        k_prep_windows16<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS,
-                                                                          mfma_bf16(b) ? 1 : 0);
+        const int bf = mfma_bf16(b) ? 1 : 0;
+        if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS, bf);
+        else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS, bf);
         HIP_TRY(hipGetLastError());
     }
     return DM_OK;
@@ -1600,6 +1602,8 @@ int dm_aggregate(const double *d_in, int32_t T, int32_t h, int32_t w, int32_t re
     const int W2 = w / 2, h2 = h / 2;
     const char *ag = getenv("DM_AGGREGATE");
     if (W2 >= 16 && 4 * W2 <= 256 && !(ag && ag[0] == '0')) { // streaming kernel
+        // band rows: what fits AGG_LDS_DOUBLES (8-row bands measured no faster at C3: the
+        // extra input row per band offsets the occupancy)
         const int BR = AGG_LDS_DOUBLES / (4 * W2) < h2 ? AGG_LDS_DOUBLES / (4 * W2) : h2;
         const size_t nwg = (size_t)T * h2 * W2 * ((h2 + BR - 1) / BR);
         if (nwg <= 0x7fffffff) {

@@ -33,6 +33,9 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 // Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
 // lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
 // GW = G/NW: one group per wave of k_level1_mfq.
+// WSC: window side known at compile time (0 = g.ws): the window's bytes are loaded once and
+// serve both the sums and the fragments.
+template <int WSC>
 __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS, int bf)
 {
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -43,14 +46,24 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
     const int q0 = (int)((idx / (16 * (size_t)G)) % g.h0);
     const int t = (int)(idx / (16 * (size_t)G * g.h0));
     const int q1 = 16 * GW * (tau / GW) + GW * c + (tau % GW);
-    const int ws = g.ws, n = ws * ws;
+    const int ws = WSC ? WSC : g.ws, n = ws * ws;
     const uint8_t *base = g.img2 + (size_t)(g.org[2 * t] + q0) * g.pitch2 + g.org[2 * t + 1] + q1;
+    int pix[WSC ? WSC * WSC : 1];
+    if constexpr (WSC != 0) {
+#pragma unroll
+        for (int k = 0; k < WSC * WSC; ++k) pix[k] = (int)base[(size_t)(k / WSC) * g.pitch2 + (k % WSC)] - 128;
+    }
+    // tap k of the window, k < n
+    auto px = [&](int k) -> int {
+        if constexpr (WSC != 0) return pix[k];
+        else return (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128;
+    };
     int s = 0, s2 = 0;
-    for (int u = 0; u < ws; ++u)
-        for (int v = 0; v < ws; ++v) {
-            const int b = (int)base[(size_t)u * g.pitch2 + v] - 128;
-            s += b; s2 += b * b;
-        }
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+        const int b = px(k);
+        s += b; s2 += b * b;
+    }
     const long long dI = (long long)n * s2 - (long long)s * s;
     float bq;
     if (g.method == DM_TM_CCOEFF) bq = 1.0f;
@@ -63,7 +76,7 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
             int w[4] = {0, 0, 0, 0};
             for (int j = 0; j < 8; ++j) {
                 const int k = 8 * hq + j;
-                const int val = k < n ? (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128 : 0;
+                const int val = k < n ? px(k) : 0;
                 w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1))); // exact in bf16
             }
             dm_v4i o;
@@ -77,8 +90,7 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
             int w[4] = {0, 0, 0, 0};
             for (int j = 0; j < 16; ++j) {
                 const int k = 64 * ks + 16 * hq + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128;
+                const int val = k < n ? px(k) : 0;
                 w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
             }
             if (KS == 1 && n <= 32 && hq >= 2) { // taps 32..63 are zero in every A row: these

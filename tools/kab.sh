@@ -7,12 +7,14 @@ TAG=$1; shift
 REPO=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$REPO/gpurun_out/kab_$TAG
 mkdir -p "$OUT"
-LIBS=(); for l in "$@"; do LIBS+=("$(cd "$(dirname "$l")" && pwd)/$(basename "$l")"); done
+# an entry may carry environment settings: lib.so+DM_AGG_BR=8+...
+LIBS=(); for l in "$@"; do f=${l%%+*}; e=${l#"$f"}; LIBS+=("$(cd "$(dirname "$f")" && pwd)/$(basename "$f")$e"); done
 cd /tmp && export TMPDIR=/tmp
 for pass in 1 2; do
-  for lib in "${LIBS[@]}"; do
-    b=$(basename "$lib" .so)
-    DM_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${b}_$pass" -o run -- \
+  for ent in "${LIBS[@]}"; do
+    lib=${ent%%+*}; envs=${ent#"$lib"}; envs=${envs//+/ }
+    b=$(basename "$lib" .so)$(echo "$envs" | tr ' =' '_-')
+    env $envs DM_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${b}_$pass" -o run -- \
         python3 "$REPO/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-volume > "$OUT/${b}_$pass.json" 2> "$OUT/${b}_$pass.err"
     python3 - "$OUT/${b}_$pass" "$b pass $pass" <<'PY'
 import csv, glob, json, sys
