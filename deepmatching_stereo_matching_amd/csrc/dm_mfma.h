@@ -665,6 +665,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         load_row(fb, q0 + 1);
         float Ca[M][4], Cb[M][4], la[4], lb[4];
         pool_cols(fa, Ca, la);
+        // row pooling, first half: the even row q0 opens level-1 row u with the previous
+        // pair's odd row (Cprev) -- folded in now (max is exact and order-free), so Cprev is
+        // dead before Cb is born and the loop carries it without a copy
+        if (q0 > 0) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Ca[m][r] = fmaxf(Cprev[m][r], Ca[m][r]);
+        }
         if constexpr (!LATE) load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
         pool_cols(fb, Cb, lb);
         if (c == 15) {
@@ -688,7 +697,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         double l1q[M]; // level-1 row u - 1, consumed by level2_row below
 #pragma unroll
         for (int m = 0; m < M; ++m) l1q[m] = l1p[m];
-        // row pooling: even row q0 opens level-1 row u, odd row q0 + 1 closes it
+        // row pooling: even row q0 (Cprev already folded in) and odd row q0 + 1 close row u
         // a constant child map (den == 0) makes its values NaN (0 * inf in the Markstein step,
         // the reference's 0/0): pow14_zf and pow14_q4 map NaN to NaN, so the sum and level 1
         // of its cell are NaN, as in the reference
@@ -699,8 +708,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             float R[4], x[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float Ra = q0 == 0 ? Ca[m][r] : fmaxf(Cprev[m][r], Ca[m][r]);
-                R[r] = fmaxf(Ra, Cb[m][r]);
+                R[r] = fmaxf(Ca[m][r], Cb[m][r]);
                 Cprev[m][r] = Cb[m][r];
             }
             // r = med3(R * a_p, lo, hi); x = (r - rmin) / den (Markstein, see norm_mk), packed
