@@ -268,6 +268,11 @@ __global__ void k_stats(Geo g, Stats s)
     s.sT[o] = sa; s.aP[o] = ap; s.sI[o] = sb; s.bQ[o] = bq;
 }
 
+// num = n * acc - sT * sI with full-rate v_mul_i32_i24 (v_mul_lo_u32 is quarter rate): every
+// operand fits 24 signed bits (n <= 225, |acc| <= 225 * 128^2 < 2^23, |sT|, |sI| <= 225 * 128)
+// and |num| <= n^2 * 128^2 < 2^31 (Cauchy-Schwarz), so the low 32 bits are the exact value
+__device__ __forceinline__ int num_of(int n, int acc, int sT, int sI) { return __mul24(n, acc) - __mul24(sT, sI); }
+
 // exact numerator for (patch p0,p1 ; window q0,q1) of tile t, read from global images
 __device__ int num_global(const Geo &g, int t, int p0, int p1, int q0, int q1, int sT, int sI)
 {
@@ -278,7 +283,7 @@ __device__ int num_global(const Geo &g, int t, int p0, int p1, int q0, int q1, i
         const uint8_t *b = g.img2 + (size_t)(ro + q0 + u) * g.pitch2 + co + q1;
         for (int v = 0; v < g.ws; ++v) acc += ((int)a[v] - 128) * ((int)b[v] - 128);
     }
-    return g.ws * g.ws * acc - sT * sI;
+    return num_of(g.ws * g.ws, acc, sT, sI);
 }
 
 // rectified level-0 value L0[p][q] (co_map_list[0]), evaluated on demand
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(K2_THREADS) void k_level1_generic(Geo g, Stats s, d
             for (int u = 0; u < WS; ++u)
 #pragma unroll
                 for (int v = 0; v < WS; ++v) a += Tr[u * WS + v] * (int)crop[(q0 + u) * Wc + q1 + v];
-            const float y = y_of_num(n * a - sT * s.sI[tb + q], s.bQ[tb + q]);
+            const float y = y_of_num(num_of(n, a, sT, s.sI[tb + q]), s.bQ[tb + q]);
             ymap[q] = y;
             ymn = fminf(ymn, y);
             ymx = fmaxf(ymx, y);
@@ -717,9 +722,10 @@ struct PatchL0 {
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < NJ; ++j) acc[i][j] = 0;
+        const uint8_t *rp0 = g.img2 + (size_t)(ro + qa0) * g.pitch2 + co + qb0;
 #pragma unroll
         for (int r = 0; r < NI + WS - 1; ++r) {
-            const uint8_t *rp = g.img2 + (size_t)(ro + qa0 + r) * g.pitch2 + co + qb0;
+            const uint8_t *rp = rp0 + (size_t)r * (unsigned)g.pitch2;
             const unsigned off = (unsigned)((uintptr_t)rp & 3u);
             const unsigned *A = (const unsigned *)(rp - off);
             unsigned D[ND + 1], E[NE + 1];
@@ -766,7 +772,7 @@ struct PatchL0 {
     __device__ double rect(const Geo &g, const Stats &s, int t, int q0, int q1, int acc) const
     {
         const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
-        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
+        const float r = r_of_y(y_of_num(num_of(WS * WS, acc, sT, s.sI[oq]), s.bQ[oq]), ap, g.method);
         return pow14((double)norm_x(r, rmn, rmx));
     }
     __device__ double value(const Geo &g, const Stats &s, int t, int q0, int q1) const
@@ -777,7 +783,7 @@ struct PatchL0 {
 #pragma unroll
         for (int k = 0; k < WS * WS; ++k) acc += tap(k) * ((int)b[(size_t)(k / WS) * g.pitch2 + (k % WS)] - 128);
         const size_t oq = (size_t)t * g.h0 * g.w0 + (size_t)q0 * g.w0 + q1;
-        const float r = r_of_y(y_of_num(WS * WS * acc - sT * s.sI[oq], s.bQ[oq]), ap, g.method);
+        const float r = r_of_y(y_of_num(num_of(WS * WS, acc, sT, s.sI[oq]), s.bQ[oq]), ap, g.method);
         return pow14((double)norm_x(r, rmn, rmx));
     }
 };
@@ -841,7 +847,7 @@ __global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, co
 #pragma unroll
                 for (int j = 0; j < 7; ++j) {
                     const size_t oq = (size_t)t * P + (size_t)(qa0 + i) * w0 + qb0 + j;
-                    yr[j] = y_of_num(n * acc[i][j] - sT * s.sI[oq], s.bQ[oq]);
+                    yr[j] = y_of_num(num_of(n, acc[i][j], sT, s.sI[oq]), s.bQ[oq]);
                 }
                 pool_row(i, yr);
             }
@@ -860,7 +866,7 @@ __global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, co
 #pragma unroll
                 for (int k = 0; k < n; ++k) acc += pt.tap(k) * ((int)b[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128);
                 const size_t oq = (size_t)t * P + (size_t)qa * w0 + qb;
-                yr[j] = y_of_num(n * acc - sT * s.sI[oq], s.bQ[oq]);
+                yr[j] = y_of_num(num_of(n, acc, sT, s.sI[oq]), s.bQ[oq]);
             }
             pool_row(i, yr);
         }
