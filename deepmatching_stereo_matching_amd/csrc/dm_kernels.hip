@@ -1122,8 +1122,8 @@ static bool mfma_bf16(const dm_tiles *b)
 // waves per workgroup of k_level1_mfq: NW = min(4, G/2); column group width GW = G/NW
 static int mfq_nw(const dm_tiles *b)
 {
-    const char *e = getenv("DM_MFQ_NWMAX"); // A/B knob: 4 or 8 waves per workgroup at most
-    const int cap = (e && e[0] == '4') ? 4 : 8;
+    const char *e = getenv("DM_MFQ_NWMAX"); // A/B knob: 2, 4 or 8 waves per workgroup at most
+    const int cap = (e && e[0] == '4') ? 4 : (e && e[0] == '2') ? 2 : 8;
     return b->w0 / 16 / 2 < cap ? b->w0 / 16 / 2 : cap;
 }
 
@@ -1283,7 +1283,9 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     }
     // register budget: 5 waves/SIMD (measured best for both variants on C3)
 #define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
-    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 4, 4) DM_MQ(1, 2, 8)
+    // GW = 4 with 4 waves: 4 waves/SIMD register budget (5 spills)
+    if (KS == 1 && GW == 4 && NW == 4) { k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 2, 8) DM_MQ(1, 4, 2)
     if constexpr (!YF) {
         DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4) DM_MQ(2, 2, 8)
         DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4) DM_MQ(3, 2, 8)
