@@ -46,6 +46,11 @@ S = 128
 GRID = 8
 CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c4': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
 C4_PAIRS = 64                  # BASELINE configs[3]: a batch of 64 independent 1024^2 pairs
+# Rehearsal of the multi-rank path on a box with fewer GPUs than ranks (tests/test_bench_ranks.py):
+# DM_BENCH_BACKEND=gloo and DM_BENCH_ONE_DEVICE=1 put every rank on cuda:0 over gloo.  The
+# driver's runs leave both unset: one rank per GPU over RCCL ("nccl").
+BACKEND = os.environ.get('DM_BENCH_BACKEND', 'nccl')
+ONE_DEVICE = os.environ.get('DM_BENCH_ONE_DEVICE', '0') == '1'
 VOLUME_BUDGET = 72e9           # bytes of level-0 volume materialised for its roofline: the whole
                                # C3 batch in float32 (68.7 GB), 8 S=256 tiles in fp16 (whole
                                # rounds of workgroups over the chip, as C5's 256 tiles are)
@@ -269,7 +274,7 @@ def launch_ranks(args):
     import socket
     import subprocess
     n = torch.cuda.device_count()
-    if n < args.gpus:
+    if n < args.gpus and not ONE_DEVICE:
         raise SystemExit('bench.py --gpus %d: only %d GPU(s) visible' % (args.gpus, n))
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
@@ -309,10 +314,15 @@ def main():
     if world != args.gpus:
         raise SystemExit('bench.py --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
     dist = world > 1
+    if ONE_DEVICE:   # rehearsal of the multi-rank path on a one-GPU box (tests only)
+        local = 0
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if BACKEND == 'nccl':
+            tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            tdist.init_process_group(BACKEND)
     dev = torch.device('cuda', local if dist else 0)
     torch.cuda.set_device(dev)
     joined = world
