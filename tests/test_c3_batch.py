@@ -1,7 +1,7 @@
-"""BASELINE config C3 exactly as bench.py runs it, against the oracle tile by tile.
+"""BASELINE configs C3 (and C2) exactly as bench.py runs them, against the oracle tile by tile.
 
-The bench's input (the 1156^2 synthetic pair of seed 1000) is cut into 8x8
-tiles of S = 128 (ws = 5) and solved as ONE batch through the path bench.py times
+The bench's input (the 1156^2 synthetic pair of seed 1000; 580^2 for C2) is
+cut into 8x8 tiles of S = 128 (S = 64) with ws = 5 and solved as ONE batch through the path bench.py times
 (TileBatch -> DevicePyramid.build: stats, the fused level-1/level-2 kernel, levels >= 3 ->
 match with sub-pixel, levels 0/1 recomputed on demand -> stitch).  All 64 tiles have their
 Matching output compared bit for bit with the oracle's (streaming mode, pinned pow; pinned
@@ -16,8 +16,7 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-S, WS, GRID = 128, 5, 8
-CHECK = [(i, j) for j in range(GRID) for i in range(GRID)]
+WS, GRID = 5, 8
 
 
 def _same(a, b):
@@ -26,7 +25,8 @@ def _same(a, b):
     assert np.array_equal(a, b, equal_nan=True), 'max |d| = %r' % np.nanmax(np.abs(a - b))
 
 
-def test_c3_batch_vs_oracle():
+@pytest.mark.parametrize('S', [128, 64])   # C3, C2
+def test_c3_batch_vs_oracle(S):
     from deepmatching_stereo_matching_amd import _lib as L
     from deepmatching_stereo_matching_amd import engine
     from deepmatching_stereo_matching_amd.synthetic import stereo_pair
@@ -44,7 +44,7 @@ def test_c3_batch_vs_oracle():
     match, dmap = match.cpu().numpy(), dmap.cpu().numpy()[0]
     O.set_pow_mode('pinned')
     try:
-        for i, j in CHECK:
+        for i, j in [(i, j) for j in range(GRID) for i in range(GRID)]:
             t = j * GRID + i                       # reference order: j outer, i inner
             r, c = org[t]
             assert (r, c) == (i * S, j * S)
