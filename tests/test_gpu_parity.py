@@ -509,3 +509,40 @@ def test_fp16_volume_flip_rate(S):
     # where the index agrees the score differs by fp16 rounding at most
     same = (m16[:, :2] == ref[:, :2]).all(dim=1)
     assert float((m16[:, 2] - ref[:, 2]).abs()[same].max()) < 1e-2
+
+
+def _sweep_cases():
+    """Seeded shapes for the on-demand matching paths: ws 1/3 (bytes only), 5/7 (one v_dot4
+    word + remainder bytes), interior (dword/dot4 window blocks) and border (byte path)
+    entries, non-square and non-power-of-two maps, both methods."""
+    from deepmatching_stereo_matching_amd.engine import pyramid_plan
+    rng = np.random.default_rng(2024)
+    cases = []
+    for ws in (1, 3, 5, 7):
+        while sum(c[2] == ws for c in cases) < 3:
+            h0 = int(rng.choice([16, 24, 32, 48, 64]))
+            w0 = int(rng.choice([16, 32, 40, 48, 64, 96]))
+            try:
+                pyramid_plan(h0, w0)   # shapes the reference's _aggregation can halve (:96-103)
+            except ValueError:
+                continue
+            cases.append((h0, w0, ws, int(rng.choice([4, 5])), int(rng.integers(1 << 20))))
+    return cases
+
+
+@pytest.mark.parametrize('h0,w0,ws,method,seed', _sweep_cases())
+def test_matching_sweep_vs_oracle(h0, w0, ws, method, seed, mirror):
+    """Levels and Matching (with sub-pixel) bit for bit against the oracle on the sweep."""
+    CM, MT, CD = mirror
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1, w0 + ws - 1, seed=seed, dx=2, max_disp=max(2, min(h0, w0) // 4),
+                       sinusoidal=True)
+    feat = 'cv2.TM_CCOEFF_NORMED' if method == 5 else 'cv2.TM_CCOEFF'
+    co = CM.Correlation_map(a, b, window_size=ws, feature_name=feat)
+    co()
+    olev, it, _ = O.pyramid(O.corr_l0(a, b, ws, feat))
+    assert co.iteration == it
+    for k in range(1, len(olev)):
+        _same(co.co_map_list[k], olev[k])
+    if len(olev) > 1:
+        _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
