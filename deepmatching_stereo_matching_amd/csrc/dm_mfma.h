@@ -612,10 +612,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
     };
 
-    // level 2 of this workgroup's cell from level-1 row u (values l1p, lane c == 15's value
-    // of wave w-1 in xch2[u & 1]): NaN-propagating MaxPool(3,2,1) of the four level-1 maps
-    // (torch semantics, misc/Correlation_map.py:101-103), sum of the four maps in ul, ur, ll,
-    // lr order (:109-122), /4, rectify; rows stream over u.
+    // level 2 of this workgroup's cell from level-1 row u: NaN-propagating MaxPool(3,2,1) of
+    // the four level-1 maps (torch semantics, misc/Correlation_map.py:101-103), sum of the four
+    // maps in ul, ur, ll, lr order (:109-122), /4, rectify; rows stream over u.  l1p holds the
+    // level-1 values BEFORE their rectification (the child sums s, level 1 = pow14(s / 4)),
+    // lane c == 15's of wave w-1 in xch2[u & 1]: pow14 is monotone non-decreasing (NaN in ->
+    // NaN out), so MaxPool of pow14(s / 4) == pow14 of MaxPool(s) / 4 bit for bit, and only
+    // the pooled value of each child is rectified -- one pow per lane per level-2 row instead
+    // of one per level-1 value.
     auto level2_row = [&](int u, const double (&l1p)[M]) {
         const double lft = __shfl(l1p[M - 1], lane - 1);
         const double left = c != 0 ? lft : (wave == 0 ? -INFINITY : xch2[u & 1][wave - 1][grp]);
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             const int u2 = u >> 1, slot = u2 % L2B;
 #pragma unroll
             for (int j = 0; j < M2; ++j) {
-                const double R2 = nanmax_d(Racc2[j], Cq[j]);
+                const double R2 = pow14_q4(nanmax_d(Racc2[j], Cq[j]), plds); // pooled child, rectified
                 Cprev2[j] = Cq[j];
                 const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
                              s3 = __shfl(R2, c + 48);
@@ -728,8 +732,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 const double pv = pow14_zf(x[r], plds);
                 sum = r == 0 ? pv : sum + pv;
             }
-            l1p[m] = pow14_q4(sum, plds); // pow14(sum / 4)
-            if (L1) Lrow[(size_t)u * w1 + M * c + m] = l1p[m];
+            // level 1 = pow14(sum / 4), rectified where it is read: here when level 1 is
+            // stored, after level 2's MaxPool otherwise (see level2_row)
+            l1p[m] = sum;
+            if (L1) Lrow[(size_t)u * w1 + M * c + m] = pow14_q4(sum, plds);
         }
         if constexpr (L2F) {
             if (u > 0) level2_row(u - 1, l1q);
