@@ -467,6 +467,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     constexpr bool LATE = L2F;
     constexpr int L2V = 4 * GW, L2B = 64 / L2V; // level-2 values per wave per row; rows per stash
     __shared__ double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: pow inputs
+    // M == 1 (one pooled column per lane, valid on even lanes): the pooled children of RB
+    // level-2 rows, [wave][row * 4 * L2V + child * L2V + column], rectified 64 at a time
+    constexpr int RB = 64 / (4 * L2V);
+    __shared__ double stash2[L2F && GW == 2 ? NW : 1][64];
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW);
     if (tid < 64) (&xch[0][0][0][0][0])[(tid >> 4) * (NW + 1) * 16 + (tid & 15)] = -INFINITY;
@@ -639,15 +643,39 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             // the wave's 4*GW level-2 values of row u2 (cell sums on lanes of group 0) go to
             // the LDS stash; every L2B rows one pow per lane rectifies them all
             const int u2 = u >> 1, slot = u2 % L2B;
+            if constexpr (M == 1) {
+                // even lanes hold the pooled children: collect RB rows, rectify all 64 entries
+                // with one pow per lane, then sum the children (ul, ur, ll, lr) per column
+                const double R2 = nanmax_d(Racc2[0], Cq[0]);
+                Cprev2[0] = Cq[0];
+                const int rb = u2 % RB;
+                if ((c & 1) == 0) stash2[wave][rb * 4 * L2V + grp * L2V + c / 2] = R2;
+                if (rb == RB - 1 || u2 == h0 / 4 - 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const double P = pow14_q4(stash2[wave][lane], plds); // stale entries: unused
+                    __builtin_amdgcn_wave_barrier();
+                    stash2[wave][lane] = P;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (lane < (rb + 1) * L2V) {
+                        const int r = lane / L2V, col = lane % L2V;
+                        const double *q = &stash2[wave][r * 4 * L2V + col];
+                        stash[wave][((u2 - rb + r) % L2B) * L2V + col] = (((q[0] + q[L2V]) + q[2 * L2V]) + q[3 * L2V]) / 4.0;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else {
 #pragma unroll
-            for (int j = 0; j < M2; ++j) {
-                const double R2 = pow14_q4(nanmax_d(Racc2[j], Cq[j]), plds); // pooled child, rectified
-                Cprev2[j] = Cq[j];
-                const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
-                             s3 = __shfl(R2, c + 48);
-                const bool valid = M == 1 ? (c & 1) == 0 : true;
-                const int col = M == 1 ? c / 2 : M2 * c + j;
-                if (grp == 0 && valid) stash[wave][slot * L2V + col] = (((s0 + s1) + s2) + s3) / 4.0;
+                for (int j = 0; j < M2; ++j) {
+                    const double R2 = pow14_q4(nanmax_d(Racc2[j], Cq[j]), plds); // pooled child, rectified
+                    Cprev2[j] = Cq[j];
+                    const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
+                                 s3 = __shfl(R2, c + 48);
+                    if (grp == 0) stash[wave][slot * L2V + M2 * c + j] = (((s0 + s1) + s2) + s3) / 4.0;
+                }
             }
             if (slot == L2B - 1 || u2 == h0 / 4 - 1) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
