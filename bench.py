@@ -59,8 +59,8 @@ VOLUME_BUDGET = 72e9           # bytes of level-0 volume materialised for its ro
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)   # the clock settles after ~3 launches
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
                     help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
                          'c4 (64 pairs of c3 per step, sharded over the ranks), c5 (4096^2, S=256)')
