@@ -61,6 +61,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)   # the clock settles after ~3 launches
+    ap.add_argument('--streams', type=int, default=1, help='HIP streams the steps rotate over')
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
                     help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
                          'c4 (64 pairs of c3 per step, sharded over the ranks), c5 (4096^2, S=256)')
@@ -93,7 +94,13 @@ class PairSolver:
                                       L.DM_TM_CCOEFF_NORMED, self.dev)
         self.ev = []
 
-    def step(self, timed=False):
+    def step(self, timed=False, stream=None):
+        """One full solve of the pair on `stream` (default: the current stream).  Every
+        device buffer belongs to this step's DevicePyramid, so steps on different streams
+        share only the read-only images."""
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self.step(timed=timed)
         from deepmatching_stereo_matching_amd import shard
         pyr = engine.DevicePyramid(self.batch, build=False)
         ev = None
@@ -348,9 +355,17 @@ def main():
     solver = solvers[0] if solvers else None
     voxels = grid * grid * float(tile) ** 4      # per pair
 
+    # --streams S: consecutive steps go to S HIP streams round-robin, so the latency-bound
+    # tail of one pair (matching on demand, levels >= 3, stitch: ~5 % of a step) runs beside
+    # the next pair's VALU-bound level kernel.  Each step still solves its pair completely.
+    streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)] if args.streams > 1 else [None]
+    nstep = [0]
+
     def step(timed=False):
+        st = streams[nstep[0] % len(streams)]
+        nstep[0] += 1
         for s in solvers:
-            s.step(timed=timed)
+            s.step(timed=timed, stream=st)
 
     for _ in range(args.warmup):
         step()
