@@ -47,15 +47,11 @@ __device__ __forceinline__ double pow14(double x)
 typedef double dm_d2 __attribute__((ext_vector_type(2)));
 // 16-B rows as one vector: ds_read_b128 (4 LDS cycles, 64 banks) instead of ds_read2_b64
 // (8 cycles, 32 banks) -- MI355X_MICROARCH.md section LDS
-#ifndef DM_POW_SPLIT
-#define DM_POW_SPLIT 0
-#endif
+// (measured: c_i on a 16-B stride, so that the c_i and (1/c_i)^y reads share one i*16
+// address, saves one VALU per pow but ran 2 % slower -- the b64 reads then use half the
+// banks -- as did splitting (1/c_i)^y into hi / lo arrays on c_i's 8-B stride)
 struct PowLds {
-#if DM_POW_SPLIT
-    double fph[DM_POWF_NT], fpl[DM_POWF_NT]; // (1/c_i)^y hi, lo: same i*8 address as fc
-#else
     dm_d2 fp[DM_POWF_NT];
-#endif
     dm_d2 gz[DM_GZ_ROWS + 1];
     dm_d2 g32[256];
     double fc[DM_POWF_NT];
@@ -65,12 +61,7 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
 {
     for (int i = tid; i < DM_POWF_NT; i += nthreads) {
         t.fc[i] = c_powf_c[i];
-#if DM_POW_SPLIT
-        t.fph[i] = c_powf_p[2 * i];
-        t.fpl[i] = c_powf_p[2 * i + 1];
-#else
         t.fp[i] = dm_d2{c_powf_p[2 * i], c_powf_p[2 * i + 1]};
-#endif
     }
     for (int k = tid; k <= DM_GZ_ROWS; k += nthreads) {
         t.gz[k] = k == DM_GZ_ROWS ? dm_d2{(double)NAN, (double)NAN}
@@ -94,12 +85,8 @@ __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const Pow
     q = fma(q, r, DM_POWF_B2);
     q = fma(q, r, DM_POWF_B1);
     q = q * r;
-#if DM_POW_SPLIT
-    const double Phi = t.fph[i], Plo = t.fpl[i];
-#else
     const dm_d2 Pr = t.fp[i];
     const double Phi = Pr.x, Plo = Pr.y;
-#endif
     const double Blo = fma(Phi, q, Plo);
     const double Ghi = G.x, Glo = G.y;
     const double Zhi = Phi * Ghi;
