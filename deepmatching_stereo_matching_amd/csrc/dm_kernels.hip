@@ -37,7 +37,7 @@ __device__ __forceinline__ double pow14(double x)
 // Fast-path tables staged in LDS by the level-1 kernels (gathers with random rows: strides
 // of 8 and 16 B spread over the banks; one 32-B row per index conflicted 4x more, measured):
 //   fc[i], fp[i] = c_i, (1/c_i)^y hi, lo                   per mantissa index
-//   gz[k]   = 2^(yE) hi, lo for E = k - 1 + EMIN (1 <= k < DM_GZ_ROWS);  gz[0] = 0 (x == 0
+//   gz[k]   = 2^(yE) as {G, g} for E = k - 1 + EMIN (1 <= k < DM_GZ_ROWS);  gz[0] = 0 (x == 0
 //             -> +0);  gz[DM_GZ_ROWS] = NaN (pow14_q4's row for a NaN input)
 //   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127); g32[255] = NaN
 //             (x = NaN -> NaN); else 0
@@ -75,7 +75,7 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
     }
 }
 
-// dm_pow14_fast's arithmetic on mantissa M in [1,2), table index i and 2^(yE) row G
+// dm_pow14_fast's arithmetic on mantissa M in [1,2), table index i and 2^(yE) row G = {G, g}
 __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
 {
     const double r = fma(M, t.fc[i], -1.0);
@@ -84,16 +84,10 @@ __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const Pow
     q = fma(q, r, DM_POWF_B3);
     q = fma(q, r, DM_POWF_B2);
     q = fma(q, r, DM_POWF_B1);
-    q = q * r;
+    q = fma(q, r, G.y);
     const dm_d2 Pr = t.fp[i];
-    const double Phi = Pr.x, Plo = Pr.y;
-    const double Blo = fma(Phi, q, Plo);
-    const double Ghi = G.x, Glo = G.y;
-    const double Zhi = Phi * Ghi;
-    double s = fma(Phi, Ghi, -Zhi);
-    s = fma(Phi, Glo, s);
-    s = fma(Blo, Ghi, s);
-    return Zhi + s;
+    const double s = fma(Pr.x, q, Pr.y) * G.x;
+    return fma(Pr.x, G.x, s);
 }
 
 // float64 input.  Exact dm_pow14 on [2^EMIN, 1] and 0; other inputs read in-bounds rows and

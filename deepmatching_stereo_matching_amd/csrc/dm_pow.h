@@ -30,7 +30,7 @@
 typedef struct dm_pow_tabs {
     const double *fc;  /* fast: [DM_POWF_NT] c_i                                 */
     const double *fp;  /* fast: [DM_POWF_NT][2] (1/c_i)^y  hi, lo                 */
-    const double *fg;  /* fast: [1 - DM_POWF_EMIN][2] 2^(yE) hi, lo, E = EMIN..0  */
+    const double *fg;  /* fast: [1 - DM_POWF_EMIN][2] 2^(yE) = G (1 + g): G, g   */
     const double *tab; /* slow: [DM_POW_NT][3] c_i, (1/c_i)^y hi, lo             */
     const double *g;   /* slow: [5][2] 2^(j/5) hi, lo                            */
 } dm_pow_tabs;
@@ -49,7 +49,9 @@ DM_HD static inline double dm_f64_bits(uint64_t b)
     return x;
 }
 
-/* fast path, x in [2^DM_POWF_EMIN, 1]: one table row, degree-5 series, one 2^(yE) row */
+/* fast path, x in [2^DM_POWF_EMIN, 1]: one table row, degree-5 series, one 2^(yE) row
+ * {G, g} with 2^(yE) = G (1 + g); g enters the series' last step, and
+ * x^y ~ G (Phi + Phi q + Plo) = fma(Phi, G, fma(Phi, q, Plo) * G) (gen_pow_tables.py) */
 DM_HD static inline double dm_pow14_fast(double x, const double *fc, const double *fp, const double *fg)
 {
     const uint64_t b = dm_bits_f64(x);
@@ -57,21 +59,17 @@ DM_HD static inline double dm_pow14_fast(double x, const double *fc, const doubl
     const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
     const int i = (int)((b >> 43) & (DM_POWF_NT - 1));
     const double r = fma(M, fc[i], -1.0);                  /* |r| <= 2^-10 */
+    const int e = E - DM_POWF_EMIN;
+    const double G = fg[2 * e], g = fg[2 * e + 1];         /* 2^(yE) = G (1 + g) */
     double q = DM_POWF_B5;
     q = fma(q, r, DM_POWF_B4);
     q = fma(q, r, DM_POWF_B3);
     q = fma(q, r, DM_POWF_B2);
     q = fma(q, r, DM_POWF_B1);
-    q = q * r;                                             /* (1+r)^y - 1 */
-    const double Phi = fp[2 * i], Plo = fp[2 * i + 1];
-    const double Blo = fma(Phi, q, Plo);                   /* M^y = Phi + Blo */
-    const int e = E - DM_POWF_EMIN;
-    const double Ghi = fg[2 * e], Glo = fg[2 * e + 1];     /* 2^(yE) */
-    const double Zhi = Phi * Ghi;
-    double s = fma(Phi, Ghi, -Zhi);
-    s = fma(Phi, Glo, s);
-    s = fma(Blo, Ghi, s);
-    return Zhi + s;
+    q = fma(q, r, g);                                      /* (1+r)^y - 1 + g */
+    const double Phi = fp[2 * i], Plo = fp[2 * i + 1];     /* (1/c_i)^y */
+    const double s = fma(Phi, q, Plo) * G;
+    return fma(Phi, G, s);
 }
 
 /* slow path: every other input (0, NaN, inf, negatives, x > 1, x < 2^EMIN) */
