@@ -55,12 +55,14 @@ struct PowLds {
     dm_d2 gz[DM_GZ_ROWS + 1];
     dm_d2 g32[256];
     double fc[DM_POWF_NT];
+    float fc32[DM_POWF_NT]; // c_i has 10 significant bits (gen_pow_tables.py): exact in float32
 };
 
 __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
 {
     for (int i = tid; i < DM_POWF_NT; i += nthreads) {
         t.fc[i] = c_powf_c[i];
+        t.fc32[i] = (float)c_powf_c[i];
         t.fp[i] = dm_d2{c_powf_p[2 * i], c_powf_p[2 * i + 1]};
     }
     for (int k = tid; k <= DM_GZ_ROWS; k += nthreads) {
@@ -75,10 +77,9 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
     }
 }
 
-// dm_pow14_fast's arithmetic on mantissa M in [1,2), table index i and 2^(yE) row G = {G, g}
-__device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
+// dm_pow14_fast's arithmetic from r = fma(M, c_i, -1), table index i and 2^(yE) row G = {G, g}
+__device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const PowLds &t)
 {
-    const double r = fma(M, t.fc[i], -1.0);
     double q = DM_POWF_B5;
     q = fma(q, r, DM_POWF_B4);
     q = fma(q, r, DM_POWF_B3);
@@ -88,6 +89,11 @@ __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const Pow
     const dm_d2 Pr = t.fp[i];
     const double s = fma(Pr.x, q, Pr.y) * G.x;
     return fma(Pr.x, G.x, s);
+}
+
+__device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
+{
+    return pow14_core_r(fma(M, t.fc[i], -1.0), i, G, t);
 }
 
 // float64 input.  Exact dm_pow14 on [2^EMIN, 1] and 0; other inputs read in-bounds rows and
@@ -120,14 +126,15 @@ __device__ __forceinline__ double pow14_q4(double s, const PowLds &t)
 // float32 input (widened exactly): exact dm_pow14((double)x) for x == 0 and for normal
 // x in [2^EMIN, 1] (f32 subnormals would need renormalising: callers never produce them);
 // NaN -> NaN (the g32 NaN row).  Fewer integer ops than pow14_zd: exponent, index and
-// mantissa come straight from the f32 bits.
+// mantissa come straight from the f32 bits, and r = M c_i - 1 is exact in float32 (24-bit M,
+// 10-bit c_i, |r| < 2^-9), so one float32 FMA forms the float64 FMA's value.
 __device__ __forceinline__ double pow14_zf(float x, const PowLds &t)
 {
     const unsigned u = __float_as_uint(x);
-    const double M = (double)__uint_as_float((u & 0x7FFFFFu) | 0x3F800000u);
+    const float M = __uint_as_float((u & 0x7FFFFFu) | 0x3F800000u);
     const int i = (int)((u >> 14) & (DM_POWF_NT - 1));
     const int be = (int)((u >> 23) & 0xFF);
-    return pow14_core(M, i, t.g32[be], t);
+    return pow14_core_r((double)__builtin_fmaf(M, t.fc32[i], -1.0f), i, t.g32[be], t);
 }
 
 __device__ __forceinline__ double pow14_lds(double x, const PowLds &t)
