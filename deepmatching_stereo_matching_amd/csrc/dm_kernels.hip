@@ -37,6 +37,7 @@ __device__ __forceinline__ double pow14(double x)
 // Fast-path tables staged in LDS by the level-1 kernels (gathers with random rows: strides
 // of 8 and 16 B spread over the banks; one 32-B row per index conflicted 4x more, measured):
 //   fc[i], fp[i] = c_i, (1/c_i)^y hi, lo                   per mantissa index
+//   fc32[i]       = c_i as float32 (exact: 10 significant bits), for float32 inputs
 //   gz[k]   = 2^(yE) as {G, g} for E = k - 1 + EMIN (1 <= k < DM_GZ_ROWS);  gz[0] = 0 (x == 0
 //             -> +0);  gz[DM_GZ_ROWS] = NaN (pow14_q4's row for a NaN input)
 //   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127); g32[255] = NaN

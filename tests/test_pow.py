@@ -59,3 +59,34 @@ def test_agrees_with_libm_mostly():
     xs = rng.random(20000)
     u = np.array([_ulps(O.pow14(x), math.pow(x, 1.4)) for x in xs])
     assert u.max() <= 1
+
+
+def _fast_c_table():
+    import os
+    import re
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        'deepmatching_stereo_matching_amd', 'csrc', 'dm_pow_tables.h')
+    text = open(path).read()
+    body = text.split('#define DM_POWF_C_INIT {', 1)[1].split('}', 1)[0]
+    return [float.fromhex(h) for h in re.findall(r'-?0x[0-9a-fA-Fp.+-]+', body)]
+
+
+def test_fast_table_makes_float32_r_exact():
+    """The level kernel forms r = M c_i - 1 for float32 inputs with one float32 FMA
+    (dm_kernels.hip pow14_zf); that equals the oracle's float64 FMA only because c_i has
+    <= 10 significant bits and |r| < 2^-9 (gen_pow_tables.py).  Check both, and the
+    exactness itself on every bin's end points and random float32 mantissas."""
+    from fractions import Fraction
+    cs = _fast_c_table()
+    assert len(cs) == 512
+    for i, c in enumerate(cs):
+        m, e = math.frexp(c)
+        assert float(m * 2 ** 10).is_integer(), (i, c)
+        for M in (1 + i / 512, 1 + (i + 1) / 512 - 2.0 ** -23):
+            assert abs(Fraction(M) * Fraction(c) - 1) < Fraction(1, 512), (i, M)
+    rng = np.random.default_rng(7)
+    for u in rng.integers(0, 1 << 23, 20000):
+        M = 1 + int(u) / 2 ** 23
+        i = int(u) >> 14
+        exact = Fraction(M) * Fraction(cs[i]) - 1
+        assert float(np.float32(float(exact))) == exact   # representable in float32
