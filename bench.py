@@ -15,7 +15,10 @@ environment launches N ranks itself through torch.distributed.run before touchin
          pairs r::N (strong scaling over the fixed batch; no collective);
   c5     one 4096^2 pair per step, its 256 tiles sharded over the ranks, results
          all-gathered (RCCL over xGMI) and stitched (strong scaling).
-Timing is barrier + synchronize bracketed, max over ranks.
+Timing is barrier + synchronize bracketed, max over ranks.  Consecutive pair solves are
+pipelined over 2 HIP streams (--streams): a solve's level kernel waits for the previous
+solve's level kernel, and the previous pair's latency-bound tail (levels >= 3, matching,
+stitch) runs beside it; every step still solves its pair completely inside the timed region.
 
 Also reported: the roofline of the dominant kernel (dm_corr_level12), timed with HIP
 events on the launch stream inside the timed steps, the HBM roofline of the level-0
@@ -61,7 +64,8 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)   # the clock settles after ~3 launches
-    ap.add_argument('--streams', type=int, default=1, help='HIP streams the steps rotate over')
+    ap.add_argument('--streams', type=int, default=2,
+                    help='HIP streams consecutive pair solves are pipelined over (1: no overlap)')
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
                     help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
                          'c4 (64 pairs of c3 per step, sharded over the ranks), c5 (4096^2, S=256)')
@@ -94,20 +98,22 @@ class PairSolver:
                                       L.DM_TM_CCOEFF_NORMED, self.dev)
         self.ev = []
 
-    def step(self, timed=False, stream=None):
+    def step(self, timed=False, stream=None, wait=None):
         """One full solve of the pair on `stream` (default: the current stream).  Every
         device buffer belongs to this step's DevicePyramid, so steps on different streams
-        share only the read-only images."""
+        share only the read-only images.  `wait`: event the level kernel waits for (the
+        previous solve's level-kernel end when solves are pipelined over streams); this
+        solve's level-kernel end is left in self.last_end."""
         if stream is not None:
             with torch.cuda.stream(stream):
-                return self.step(timed=timed)
+                return self.step(timed=timed, wait=wait)
         from deepmatching_stereo_matching_amd import shard
         pyr = engine.DevicePyramid(self.batch, build=False)
-        ev = None
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         if timed:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev.append(ev)
-        pyr.build(events=ev)               # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
+        self.last_end = ev[1]
+        pyr.build(events=ev, wait=wait)    # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
         match = pyr.match(sub_pix=True)
         if self.world > 1:
             match = shard._gather_units(match, self.T, self.rank, self.world, match.shape[1:], match.dtype)
@@ -355,17 +361,24 @@ def main():
     solver = solvers[0] if solvers else None
     voxels = grid * grid * float(tile) ** 4      # per pair
 
-    # --streams S: consecutive steps go to S HIP streams round-robin, so the latency-bound
-    # tail of one pair (matching on demand, levels >= 3, stitch: ~5 % of a step) runs beside
-    # the next pair's VALU-bound level kernel.  Each step still solves its pair completely.
-    streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)] if args.streams > 1 else [None]
-    nstep = [0]
+    # --streams S: consecutive pair solves go to S HIP streams round-robin, pipelined: each
+    # solve's level kernel waits for the previous solve's level kernel (so level kernels never
+    # share the GPU with each other and each one's event time stays its own), while the
+    # previous pair's latency-bound tail (levels >= 3, matching on demand, stitch: ~5 % of a
+    # solve) runs beside it.  Each solve still solves its pair completely.
+    # c5 split over ranks all-gathers inside every solve: its collectives stay on one stream
+    # (RCCL operations of one communicator must not race each other on two streams)
+    nstreams = 1 if split else max(1, args.streams)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)] if nstreams > 1 else [None]
+    nsolve = [0]
+    prev_end = [None]
 
     def step(timed=False):
-        st = streams[nstep[0] % len(streams)]
-        nstep[0] += 1
         for s in solvers:
-            s.step(timed=timed, stream=st)
+            st = streams[nsolve[0] % len(streams)]
+            nsolve[0] += 1
+            s.step(timed=timed, stream=st, wait=prev_end[0] if st is not None else None)
+            prev_end[0] = s.last_end
 
     for _ in range(args.warmup):
         step()
@@ -414,7 +427,8 @@ def main():
                'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
                'config': {'workload': workload, 'tile': tile, 'tiles_per_pair': grid * grid,
                           'window_size': WS, 'pairs_per_step': job_pairs,
-                          'pairs_per_gpu_per_step': per_gpu, 'parallelism': par},
+                          'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
+                          'streams': nstreams},
                'roofline': roof}
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)

@@ -151,15 +151,21 @@ class DevicePyramid:
         self._have_minmax = True
         return l1
 
-    def build(self, events=None):
+    def build(self, events=None, wait=None):
         """Levels >= 1.  ``events``: optional (start, end) torch.cuda.Event pair recorded
-        around the level-1 (or fused level-1/level-2) kernel on this pyramid's stream."""
+        around the level-1 (or fused level-1/level-2) kernel on this pyramid's stream.
+        ``wait``: optional event the level kernel waits for (the stats run before it) -- a
+        caller pipelining pairs over streams passes the previous pair's level-kernel end, so
+        the level kernels run one after another while each pair's latency-bound tail
+        (levels >= 3, matching, stitch) overlaps the next pair's level kernel."""
         b, lib = self.b, self.lib
         self.compute_stats()
         if self.nlev > 1 and len(self.levels) == 1:
             h, w = b.h0 // 2, b.w0 // 2
             fused = False
             st = self.stream if self.stream is not None else torch.cuda.current_stream()
+            if wait is not None:
+                st.wait_event(wait)
             if events:
                 events[0].record(st)
             if self.fuse_level2 and self.nlev >= 3:
