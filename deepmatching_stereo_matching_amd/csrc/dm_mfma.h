@@ -29,7 +29,9 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 // ===================================================================================
 
 // Bw16[t][q0][tau][ks][lane] (16 B): lane L = c + 16 hq holds taps k = 64 ks + 16 hq + j of
-// window (q0, G*c + tau);  QS16[t][q0][tau][c] = { bits(f32(-sum(I'))), bits(b_q) }.
+// window (q0, G*c + tau) -- or, spread layout (KS == 1, n <= 32), taps 8 hq + j (j < 8) in
+// bytes 0..7 and the window's {qx, qy} in words 2, 3 (build_a places A's taps the same way);
+// QS16[t][q0][tau][c] = { bits(f32(-sum(I'))), bits(b_q) }.
 // Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
 // lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
 // GW = G/NW: one group per wave of k_level1_mfq.
@@ -85,17 +87,28 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
         }
         return;
     }
+    // spread layout (KS == 1, n <= 32; build_a uses the same): lane c + 16 hq holds taps
+    // 8 hq .. 8 hq + 7 in bytes 0..7 and the window's stats {qx, qy} in words 2, 3, which meet
+    // A's zero bytes 8..15 -- every lane reads its own window's stats from its own fragment
+    // (qs_of_frag), no cross-lane move
+    const bool spread = KS == 1 && n <= 32;
     for (int ks = 0; ks < KS; ++ks)
         for (int hq = 0; hq < 4; ++hq) {
             int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 64 * ks + 16 * hq + j;
-                const int val = k < n ? px(k) : 0;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            if (KS == 1 && n <= 32 && hq >= 2) { // taps 32..63 are zero in every A row: these
-                w[0] = w[3] = qx;                // lanes carry the window's stats instead
-                w[1] = w[2] = qy;                // (qs_of_frag: one 16-B load per lane per tile)
+            if (spread) {
+                for (int j = 0; j < 8; ++j) {
+                    const int k = 8 * hq + j;
+                    const int val = k < n ? px(k) : 0;
+                    w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+                }
+                w[2] = qx;
+                w[3] = qy;
+            } else {
+                for (int j = 0; j < 16; ++j) {
+                    const int k = 64 * ks + 16 * hq + j;
+                    const int val = k < n ? px(k) : 0;
+                    w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+                }
             }
             dm_v4i o;
             o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
@@ -103,19 +116,15 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
         }
 }
 
-// Window stats of this lane's window from its own B fragment (KS == 1, n <= 32, i8): lanes
-// 32..63 (taps 32..63, multiplied by A's zero padding) hold {qx, qy, qy, qx}, qx = f32 bits
-// of -sum(I'), qy = b_q of window c.  v_permlane32_swap(vdst = b.w, vsrc = b.x) leaves vsrc =
-// {b.w rows 2, 3 ; b.x rows 2, 3} = qx in every row (same for b.y / b.z -> qy).  The results
-// sit in b.x and b.z, the LOW halves of register pairs, which the packed y arithmetic
-// broadcasts with op_sel_hi = 0 in place -- no copies; the fragment is dead after its MFMA.
-// (k_volume_ls reads {qx, qy} as one aligned 8-B pair at the row's start instead.)
+// Window stats of this lane's window from its own B fragment (spread layout: KS == 1,
+// n <= 32, i8): words 2, 3 = {qx, qy}, qx = f32 bits of -sum(I'), qy = b_q of window c --
+// an aligned register pair whose halves the packed y arithmetic broadcasts with op_sel.
+// (Round 2 first carried them in lanes 32..63 only and moved them with two
+// v_permlane32_swap per tile: 8 issue cycles each on gfx950, tools/valu_probe.hip.)
 typedef float dm_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ dm_f2 qs_of_frag(const dm_v4i &b)
 {
-    const auto x = __builtin_amdgcn_permlane32_swap((unsigned)b.w, (unsigned)b.x, false, false);
-    const auto y = __builtin_amdgcn_permlane32_swap((unsigned)b.y, (unsigned)b.z, false, false);
-    return dm_f2{__uint_as_float(x[1]), __uint_as_float(y[1])};
+    return dm_f2{__int_as_float(b.z), __int_as_float(b.w)};
 }
 __device__ __forceinline__ dm_f2 qs_pair(int2 q) { return dm_f2{__int_as_float(q.x), __int_as_float(q.y)}; }
 // (measured: the same through ds_bpermute -- LDS instead of VALU issue -- ran 4 % slower in
@@ -203,6 +212,13 @@ __device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, 
                 const int val = k < n ? (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128 : 0;
                 w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1)));
             }
+        } else if (KS == 1 && n <= 32) { // spread layout (k_prep_windows16): taps 8 grp + j
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * grp + j;
+                int val = 0;
+                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
+                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+            }
         } else {
             for (int j = 0; j < 16; ++j) {
                 const int k = 64 * ks + 16 * grp + j;
@@ -279,24 +295,10 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
     const size_t tb = (size_t)t * P;
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
-    // A operand: patch row rho = c: cell rho>>2, child rho&3; taps k = 64 ks + 16 grp + j
+    // A operand: patch row rho = c: cell rho>>2, child rho&3 (build_a: the tap layout of
+    // k_prep_windows16's fragments)
     dm_v4i A[KS];
-    {
-        const int cl = c >> 2, ch = c & 3;
-        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
-        const uint8_t *base = g.img1 + (size_t)(ro + p0) * g.pitch1 + co + p1;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 16; ++j) {
-                const int k = 64 * ks + 16 * grp + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
-            }
-            A[ks].x = w[0]; A[ks].y = w[1]; A[ks].z = w[2]; A[ks].w = w[3];
-        }
-    }
+    build_a<KS, false>(A, g, t, I0, J0, c, grp);
     // this lane's cell (grp) and its 4 children (acc[reg], reg = child)
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4], pidx[4];
@@ -1197,10 +1199,10 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         }
     };
     // tile tau of the row in buffer buf: MFMA + y of this lane's 4 patches (the window stats
-    // ride in the tile's lanes 32..63: read from the stage at lane 32 + c's slot)
+    // ride in words 2, 3 of the lane's own fragment: spread layout, qs_of_frag)
     auto tile_y = [&](int buf, int tau, float *y) {
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
-        const dm_f2 q2 = *(const dm_f2 *)&lds[buf * BUF + tau * 1024 + (32 + c) * 16]; // {qx, qy}
+        const dm_f2 q2 = qs_of_frag(bf); // {qx, qy}
         dm_v4i bfr[1] = {bf};
         y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, q2, n, y);
     };

@@ -8,10 +8,14 @@
 typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int ITER = 4096, CH = 8;
 
+__device__ long long g_clk[4];
+
 template <int K>
 __global__ __launch_bounds__(256) void probe(float *out, float a, float b)
 {
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    long long c0 = 0, w0 = 0;
+    if (tid == 0) { c0 = clock64(); w0 = wall_clock64(); }
     if constexpr (K == 0) { // f32 fma
         float v[CH];
         for (int c = 0; c < CH; ++c) v[c] = tid * 1e-9f + c;
@@ -65,6 +69,63 @@ __global__ __launch_bounds__(256) void probe(float *out, float a, float b)
         float s = 0; for (int c = 0; c < CH; ++c) s += v[c];
         out[tid] = s + a;
     }
+    if (tid == 0) { g_clk[0] = clock64() - c0; g_clk[1] = wall_clock64() - w0; }
+}
+
+// one VALU instruction per chain step, 8 independent chains (v = op(v, a, b))
+#define ASM_PROBE(NAME, INSN)                                                                    \
+    __global__ __launch_bounds__(256) void NAME(float *out, float a, float b)                     \
+    {                                                                                            \
+        const int tid = blockIdx.x * blockDim.x + threadIdx.x;                                   \
+        long long c0 = 0, w0 = 0;                                                                \
+        if (tid == 0) { c0 = clock64(); w0 = wall_clock64(); }                                   \
+        float v[CH];                                                                             \
+        for (int c = 0; c < CH; ++c) v[c] = tid * 1e-9f + c;                                     \
+        for (int it = 0; it < ITER; ++it)                                                        \
+            _Pragma("unroll") for (int c = 0; c < CH; ++c) asm volatile(INSN : "+v"(v[c]) : "v"(a), "v"(b)); \
+        float s = 0;                                                                             \
+        for (int c = 0; c < CH; ++c) s += v[c];                                                  \
+        out[tid] = s;                                                                            \
+        if (tid == 0) { g_clk[0] = clock64() - c0; g_clk[1] = wall_clock64() - w0; }             \
+    }
+ASM_PROBE(p_mul_f32, "v_mul_f32 %0, %0, %1")
+ASM_PROBE(p_add_f32, "v_add_f32 %0, %0, %1")
+ASM_PROBE(p_max3_f32, "v_max3_f32 %0, %0, %1, %2")
+ASM_PROBE(p_med3_f32, "v_med3_f32 %0, %0, %1, %2")
+ASM_PROBE(p_max_f32, "v_max_f32 %0, %0, %1")
+ASM_PROBE(p_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+ASM_PROBE(p_and_b32, "v_and_b32 %0, %0, %1")
+ASM_PROBE(p_lshr_b32, "v_lshrrev_b32 %0, 3, %0")
+ASM_PROBE(p_and_or_b32, "v_and_or_b32 %0, %0, %1, %2")
+ASM_PROBE(p_lshl_add_u32, "v_lshl_add_u32 %0, %0, 2, %1")
+ASM_PROBE(p_bfe_u32, "v_bfe_u32 %0, %0, 3, 9")
+ASM_PROBE(p_mov_dpp, "v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf")
+ASM_PROBE(p_permlane32, "v_permlane32_swap_b32 %0, %0")
+ASM_PROBE(p_cvt_f32_i32, "v_cvt_f32_i32 %0, %0")
+ASM_PROBE(p_mul_lo_u32, "v_mul_lo_u32 %0, %0, %1")
+ASM_PROBE(p_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %2")
+
+static void run_k(const char *name, void (*k)(float *, float, float), float *d)
+{
+    const int blocks = 256 * 8 * 4;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    k<<<blocks, 256>>>(d, 1.0000001f, 1e-7f);
+    hipEventRecord(e0);
+    k<<<blocks, 256>>>(d, 1.0000001f, 1e-7f);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double insts = blocks * 4.0 * ITER * CH;
+    long long clk[4];
+    hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_clk), sizeof(clk));
+    int wclk = 0;
+    hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);
+    const double ghz = (double)clk[0] / ((double)clk[1] / (wclk * 1e3)) / 1e9;
+    const double ns = ms * 1e6 / (insts / 1024.0);
+    printf("%-14s %8.3f ms  %.3f ns/wave-inst/SIMD  block-0 clock %.2f GHz -> %.2f cycles\n", name, ms, ns, ghz,
+           ns * ghz);
 }
 
 template <int K>
@@ -82,8 +143,14 @@ static void run(const char *name, int insts_per_iter_chain, float *d)
     hipEventElapsedTime(&ms, e0, e1);
     const double waves = blocks * 4.0, insts = waves * ITER * CH * insts_per_iter_chain;
     // 1024 SIMDs; per-SIMD ns per wave-instruction
-    printf("%-10s %8.3f ms  %.3f ns/wave-inst/SIMD  (%.2f G wave-inst/s)\n", name, ms,
-           ms * 1e6 / (insts / 1024.0), insts / (ms * 1e6));
+    long long clk[4];
+    hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_clk), sizeof(clk));
+    int wclk = 0;
+    hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0); // kHz
+    const double ghz = (double)clk[0] / ((double)clk[1] / (wclk * 1e3)) / 1e9;
+    const double ns = ms * 1e6 / (insts / 1024.0);
+    printf("%-12s %8.3f ms  %.3f ns/wave-inst/SIMD  block-0 clock %.2f GHz -> %.2f cycles\n", name, ms, ns,
+           ghz, ns * ghz);
 }
 
 int main()
@@ -96,6 +163,22 @@ int main()
     run<3>("f64_mul", 1, d);
     run<4>("i32_xor_add", 2, d);
     run<5>("cvt_f32_f64", 2, d);
+    run_k("mul_f32", p_mul_f32, d);
+    run_k("add_f32", p_add_f32, d);
+    run_k("max_f32", p_max_f32, d);
+    run_k("max3_f32", p_max3_f32, d);
+    run_k("med3_f32", p_med3_f32, d);
+    run_k("cndmask_b32", p_cndmask, d);
+    run_k("and_b32", p_and_b32, d);
+    run_k("lshrrev_b32", p_lshr_b32, d);
+    run_k("and_or_b32", p_and_or_b32, d);
+    run_k("lshl_add_u32", p_lshl_add_u32, d);
+    run_k("bfe_u32", p_bfe_u32, d);
+    run_k("mov_b32_dpp", p_mov_dpp, d);
+    run_k("permlane32_swap", p_permlane32, d);
+    run_k("cvt_f32_i32", p_cvt_f32_i32, d);
+    run_k("mul_lo_u32", p_mul_lo_u32, d);
+    run_k("mad_u32_u24", p_mad_u32_u24, d);
     hipFree(d);
     return 0;
 }
