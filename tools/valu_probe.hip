@@ -104,6 +104,9 @@ ASM_PROBE(p_permlane32, "v_permlane32_swap_b32 %0, %0")
 ASM_PROBE(p_cvt_f32_i32, "v_cvt_f32_i32 %0, %0")
 ASM_PROBE(p_mul_lo_u32, "v_mul_lo_u32 %0, %0, %1")
 ASM_PROBE(p_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %2")
+ASM_PROBE(p_and_lit, "v_and_b32 %0, 0xff0, %0")
+ASM_PROBE(p_mul_inl, "v_mul_f32 %0, 0.5, %0")
+ASM_PROBE(p_mov_b32, "v_mov_b32 %0, %1")
 
 static void run_k(const char *name, void (*k)(float *, float, float), float *d)
 {
@@ -179,6 +182,9 @@ int main()
     run_k("cvt_f32_i32", p_cvt_f32_i32, d);
     run_k("mul_lo_u32", p_mul_lo_u32, d);
     run_k("mad_u32_u24", p_mad_u32_u24, d);
+    run_k("and_b32 lit", p_and_lit, d);
+    run_k("mul_f32 inl", p_mul_inl, d);
+    run_k("mov_b32", p_mov_b32, d);
     hipFree(d);
     return 0;
 }
