@@ -151,44 +151,47 @@ class DevicePyramid:
         self._have_minmax = True
         return l1
 
-    def build(self, events=None, wait=None):
-        """Levels >= 1.  ``events``: optional (start, end) torch.cuda.Event pair recorded
-        around the level-1 (or fused level-1/level-2) kernel on this pyramid's stream.
-        ``wait``: optional event the level kernel waits for (the stats run before it) -- a
-        caller pipelining pairs over streams passes the previous pair's level-kernel end, so
-        the level kernels run one after another while each pair's latency-bound tail
-        (levels >= 3, matching, stitch) overlaps the next pair's level kernel."""
+    def build(self, events=None, wait=None, nlev=None):
+        """Levels >= 1 up to level ``nlev`` - 1 (default: the full pyramid, as
+        Correlation_map always builds it; a smaller ``nlev`` is the k-level pyramid of
+        BASELINE configs C2/C3, whose levels above k - 1 Matching never reads).  ``events``:
+        optional (start, end) torch.cuda.Event pair recorded around the level-1 (or fused
+        level-1/level-2) kernel on this pyramid's stream.  ``wait``: optional event the level
+        kernel waits for (the stats run before it) -- a caller pipelining pairs over streams
+        passes the previous pair's level-kernel end, so the level kernels run one after
+        another while each pair's latency-bound tail (levels >= 3, matching, stitch) overlaps
+        the next pair's level kernel.  Building more levels later extends the pyramid."""
         b, lib = self.b, self.lib
         self.compute_stats()
-        if self.nlev > 1 and len(self.levels) == 1:
-            h, w = b.h0 // 2, b.w0 // 2
+        top = self.nlev if nlev is None else max(1, min(int(nlev), self.nlev))
+        if top > 1 and len(self.levels) == 1:
             fused = False
             st = self.stream if self.stream is not None else torch.cuda.current_stream()
             if wait is not None:
                 st.wait_event(wait)
             if events:
                 events[0].record(st)
-            if self.fuse_level2 and self.nlev >= 3:
+            if self.fuse_level2 and top >= 3:
                 l2 = self._empty_level(2)
                 l1 = self._empty_level(1) if self.fuse_level2 == 1 else None
                 rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), L.ptr(l1), L.ptr(l2), self._s())
                 if rc == L.DM_OK:
                     self.levels += [l1, l2]
                     self._have_minmax = True
-                    h, w, fused = h // 2, w // 2, True
+                    fused = True
                 elif rc != L.DM_ERR_UNSUPPORTED:
                     L.check(rc, 'dm_corr_level12')
             if not fused:
                 self.levels.append(self._level1())
             if events:
                 events[1].record(st)
-            for _ in range(len(self.levels), self.nlev):
-                P2 = (h // 2) * (w // 2)
-                nxt = torch.empty((b.T, P2, P2), dtype=torch.float64, device=b.device)
-                L.check(lib.dm_aggregate(L.ptr(self.levels[-1]), b.T, h, w, 1, L.ptr(nxt),
-                                         self._s()), 'dm_aggregate')
-                self.levels.append(nxt)
-                h, w = h // 2, w // 2
+        while len(self.levels) < top:
+            k = len(self.levels)               # build level k from level k - 1
+            h, w = b.h0 >> (k - 1), b.w0 >> (k - 1)
+            nxt = self._empty_level(k)
+            L.check(lib.dm_aggregate(L.ptr(self.levels[k - 1]), b.T, h, w, 1, L.ptr(nxt),
+                                     self._s()), 'dm_aggregate')
+            self.levels.append(nxt)
         return self
 
     def level_shape(self, k):
@@ -249,6 +252,8 @@ class DevicePyramid:
         if not 0 <= k < self.nlev:
             raise IndexError('list index out of range')
         if k > 0:
+            if k >= len(self.levels):          # a k-level build: extend it
+                self.build(nlev=k + 1)
             if self.levels[k] is None:   # level 1 kept on chip by dm_corr_level12
                 self.levels[k] = self._level1()
             return self.levels[k]
@@ -258,22 +263,33 @@ class DevicePyramid:
         return out
 
     def match(self, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
-              filtering_mode='median', levels=None):
+              filtering_mode='median', levels=None, nlev=None):
         """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score).
         ``levels``: an explicit co_map_list (e.g. materialized_levels()) to match on
-        instead of this pyramid's (level 0 then read from memory, not re-derived)."""
+        instead of this pyramid's (level 0 then read from memory, not re-derived).
+        ``nlev``: match on the first ``nlev`` levels only, the reference's Matching on a
+        co_map_list cut to k levels with N_map = 2^(k-1): the descent
+        starts at level nlev - 1, one start per cell of that level (Matching.py:80-96)."""
         b = self.b
-        if levels is None and not self._have_minmax:
-            self.volume()
+        n = self.nlev if nlev is None else int(nlev)
+        if not 1 <= n <= self.nlev:
+            raise IndexError('list index out of range')
+        if levels is None:
+            if not self._have_minmax:
+                self.volume()
+            for k in range(len(self.levels), n):
+                self.level(k)
+            if n == 2 and self.levels[1] is None:   # the top level must be stored
+                self.level(1)
         out = torch.empty((b.T, 3, b.h0, b.w0), dtype=torch.float64, device=b.device)
         scratch = torch.empty_like(out)
         if levels is not None:
-            ptrs = (ctypes.c_void_p * self.nlev)(*[t.data_ptr() for t in levels])
+            ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in levels[:n]])
         else:
-            ptrs = (ctypes.c_void_p * self.nlev)(*([None] + [None if t is None else t.data_ptr()
-                                                              for t in self.levels[1:]]))
+            ptrs = (ctypes.c_void_p * n)(*([None] + [None if t is None else t.data_ptr()
+                                                      for t in self.levels[1:n]]))
         fnum = int(filtering_num) if filtering else 0
-        L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, self.nlev, b.T, b.h0, b.w0,
+        L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, n, b.T, b.h0, b.w0,
                                   int(bool(sub_pix)), int(filter_window_size), fnum,
                                   1 if filtering_mode == 'median' else 0,
                                   L.ptr(scratch), L.ptr(out), self._s()), 'dm_match')

@@ -1,12 +1,15 @@
 """Correlation_map mirror (reference: misc/Correlation_map.py:29-184) on gfx950 kernels.
 
-Same constructor, attributes and methods.  ``__call__`` builds the pyramid on the GPU
-with the fused level-0 -> level-1 kernel (dm_corr_level1) and dm_aggregate for the
-levels above; ``co_map_list`` is a lazy sequence whose items are materialised to numpy
-float64 (h, w, h, w) only when indexed, and ``co_map`` (the min-max level-0 volume) only
-when read.  ``Matching`` recognises the device pyramid and matches without copying.
+Same constructor, attributes and methods.  ``__call__`` builds the pyramid on the GPU:
+dm_corr_level12 evaluates levels 0 -> 1 -> 2 in one pass (level 2 written; levels 0 and 1
+stay on chip and are re-derived on request) and dm_aggregate builds the levels above.
+``co_map_list`` is a lazy sequence whose items are materialised to numpy float64
+(h, w, h, w) only when indexed, and ``co_map`` (the min-max level-0 volume) only when read.
+``Matching`` recognises the device pyramid (also cut to its first k levels) and matches
+without copying.
 """
 
+import operator
 import sys
 from collections.abc import Sequence
 
@@ -21,30 +24,70 @@ from deepmatching_stereo_matching_amd.misc.Feature_value import Feature_value
 
 
 class LevelList(Sequence):
-    """co_map_list backed by a DevicePyramid (one tile)."""
+    """co_map_list backed by a DevicePyramid (one tile).
 
-    def __init__(self, pyr):
+    Behaves like the reference's plain list where callers touch it: indexing materialises a
+    level to numpy; a prefix slice (``co_map_list[:k]``, the SURVEY.md section 0 way of asking
+    for a k-level pyramid) stays a device-backed LevelList of the first k levels, and so do
+    ``del co_map_list[k:]`` and ``pop()``; any other slice is a plain list of arrays."""
+
+    def __init__(self, pyr, n=None):
         self._pyr = pyr
+        self._n = pyr.nlev if n is None else int(n)
         self._cache = {}
 
-    def __len__(self):
-        return self._pyr.nlev
+    @property
+    def pyramid(self):
+        return self._pyr
 
-    def __getitem__(self, k):
-        if isinstance(k, slice):
-            return [self[i] for i in range(*k.indices(len(self)))]
+    def __len__(self):
+        return self._n
+
+    def _index(self, k):
+        k = operator.index(k)
         if k < 0:
             k += len(self)
         if not 0 <= k < len(self):
             raise IndexError('list index out of range')
+        return k
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            start, stop, step = k.indices(len(self))
+            if start == 0 and step == 1:
+                view = LevelList(self._pyr, max(stop, 0))
+                view._cache = self._cache
+                return view
+            return [self[i] for i in range(start, stop, step)]
+        k = self._index(k)
         if k not in self._cache:
             t = self._pyr.level(k)[0]
             self._cache[k] = t.reshape(self._pyr.level_shape(k)).cpu().numpy()
         return self._cache[k]
 
+    def __delitem__(self, k):
+        if isinstance(k, slice):
+            start, stop, step = k.indices(len(self))
+            if step == 1 and stop >= len(self) and start < len(self):
+                self._n = start
+                return
+            if start >= stop:
+                return
+        elif self._index(k) == len(self) - 1:
+            self._n -= 1
+            return
+        raise TypeError('co_map_list backed by the device pyramid can only drop its top levels')
+
+    def pop(self, k=-1):
+        if self._index(k) != len(self) - 1:
+            raise TypeError('co_map_list backed by the device pyramid can only drop its top levels')
+        top = self[len(self) - 1]
+        self._n -= 1
+        return top
+
     def device(self, k):
         """Level k as a float64 device tensor [Pk][Pk] (no host copy)."""
-        return self._pyr.level(k)[0]
+        return self._pyr.level(self._index(k))[0]
 
 
 class Correlation_map():

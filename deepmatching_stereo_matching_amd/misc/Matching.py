@@ -1,9 +1,12 @@
 """Matching mirror (reference: misc/Matching.py:20-268), backtracking on gfx950 kernels.
 
 ``__call__`` runs the whole coarse-to-fine descent (_initial_move_map, _B / _calc_match,
-optional _filter, _sub_pix_cal) in dm_match.  On a GPU-backed ``Correlation_map`` level 0
-is re-evaluated on demand from the images (never materialised); for any other object
-with a ``co_map_list`` the levels are uploaded and matched as given.
+optional _filter, _sub_pix_cal) in dm_match.  It reads ``co_map_list`` and ``N_map`` the
+way the reference does (Matching.py:85,96,105-106,127,133-134,182): the descent starts at
+``co_map_list[-1]`` and takes one step per halving of ``N_map``, so a list cut to k levels
+with N_map = 2^(k-1) is a k-level pyramid.  On a GPU-backed ``Correlation_map`` level 0
+(and level 1) is re-evaluated on demand from the images (never materialised); for any
+other object with a ``co_map_list`` the levels are uploaded and matched as given.
 """
 
 import sys
@@ -62,18 +65,46 @@ class Matching():
             diff = 0
         return diff
 
+    def _descent(self):
+        """(co_map_list, bottom, steps) of the reference's loop: _initial_move_map on
+        co_map_list[-1] with N = N_map (:85-96), then one _B per halving of N until N == 1,
+        _B number s reading co_map_list[-1 - s] (:105-106, :127, :133-134, :146-149).  A list
+        cut to k levels with N_map = 2^(k-1) descends to level 0; a
+        N_map that needs more levels than the list holds raises the reference's IndexError."""
+        lst = self.obj.co_map_list
+        n = len(lst)
+        N = self.obj.N_map
+        steps = 0
+        while True:
+            steps += 1
+            if steps > n - 1:
+                raise IndexError('list index out of range')
+            N = int(N / 2)
+            if N == 1:
+                return lst, n - 1 - steps, steps
+
     def _device_match(self):
-        pyr = getattr(self.obj, '_pyr', None)
-        nlev = len(self.obj.co_map_list)
+        lst, bottom, steps = self._descent()
+        n = len(lst)
         fnum = self.filtering_num if self.filtering else 0
-        if isinstance(pyr, engine.DevicePyramid):
+        if bottom > 0 and self.sub_pix:
+            # the reference would refine a level-`bottom` map against co_map_list[0]; not
+            # provided (DESIGN.md section 8, deviations)
+            raise NotImplementedError('Matching: N_map = %d stops the descent at level %d of %d; '
+                                      'sub_pix needs it to reach level 0' % (self.obj.N_map, bottom, n))
+        pyr = getattr(lst, 'pyramid', None)
+        if isinstance(pyr, engine.DevicePyramid) and bottom == 0:
             out = pyr.match(self.sub_pix, self.filtering, self.filter_window_size, fnum,
-                            self.filtering_mode)[0]
+                            self.filtering_mode, nlev=n)[0]
+        elif isinstance(pyr, engine.DevicePyramid):
+            levels = [lst.device(k).reshape(pyr.level_shape(k)) for k in range(bottom, n)]
+            out = engine.match_levels(levels, self.sub_pix, self.filtering, self.filter_window_size,
+                                      fnum, self.filtering_mode)
         else:
-            out = engine.match_levels(list(self.obj.co_map_list), self.sub_pix, self.filtering,
+            out = engine.match_levels([lst[k] for k in range(bottom, n)], self.sub_pix, self.filtering,
                                       self.filter_window_size, fnum, self.filtering_mode)
         if self.filtering:  # _initial_move_map / _B decrement it once per level (:91-93, :136-138)
-            self.filtering_num = max(0, self.filtering_num - nlev)
+            self.filtering_num = max(0, self.filtering_num - (steps + 1))
         return out
 
     def __call__(self):

@@ -114,6 +114,7 @@ def test_matching_on_materialised_levels(case, mirror):
 
     class Plain:
         co_map_list = olev
+        N_map = 2 ** (len(olev) - 1)
     _same(MT.Matching(Plain())(), O.match(olev, sub_pix=True))
 
 

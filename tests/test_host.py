@@ -144,3 +144,64 @@ def test_atomic_patch_on_host_matches_reference():
         assert np.array_equal(co.atomic_patch, g['atomic_patch'])
         with pytest.raises(AttributeError):      # no co_map before _create_simple_initial_co_map
             co.co_map
+
+
+def test_matching_descent_reads_co_map_list_and_n_map():
+    """Matching follows the reference's loop (misc/Matching.py:85-149): start at
+    co_map_list[-1], one _B per halving of N_map until N == 1, IndexError when N_map asks for
+    more levels than the list holds (a k-level cut: co_map_list[:k], N_map = 2^(k-1))."""
+    from deepmatching_stereo_matching_amd.misc.Matching import Matching
+
+    def obj(n, N):
+        class O:
+            co_map_list = [np.zeros((1 << (n - 1 - k),) * 4) for k in range(n)]
+            N_map = N
+        return O()
+    for n in range(2, 9):
+        lst, bottom, steps = Matching(obj(n, 2 ** (n - 1)))._descent()
+        assert (bottom, steps, len(lst)) == (0, n - 1, n)
+    assert Matching(obj(4, 4))._descent()[1:] == (1, 2)     # stops above level 0
+    assert Matching(obj(4, 6))._descent()[1:] == (1, 2)     # int(6/2) = 3, int(3/2) = 1
+    for N in (16, 1, 0):                                    # never reaches 1 in time
+        with pytest.raises(IndexError):
+            Matching(obj(4, N))._descent()
+    with pytest.raises(IndexError):
+        Matching(obj(1, 1))._descent()
+
+    class NoN:
+        co_map_list = []
+    with pytest.raises(AttributeError):
+        Matching(NoN())._descent()
+
+
+def test_level_list_cuts_like_a_list():
+    """co_map_list of the device pyramid: prefix slices stay device-backed, del of a suffix
+    and pop() shorten it, other cuts raise (host logic only, a stand-in pyramid)."""
+    from deepmatching_stereo_matching_amd.misc.Correlation_map import LevelList
+
+    class Pyr:
+        nlev = 5
+
+        def level_shape(self, k):
+            return (1 << (4 - k),) * 4
+
+        def level(self, k):
+            import torch
+            return torch.full((1,) + (1 << (2 * (4 - k)),) * 2, float(k), dtype=torch.float64)
+    ll = LevelList(Pyr())
+    assert len(ll) == 5 and ll[-1].shape == (1, 1, 1, 1) and ll[4][0, 0, 0, 0] == 4
+    v = ll[:3]
+    assert isinstance(v, LevelList) and len(v) == 3 and v[-1][0, 0, 0, 0] == 2
+    assert isinstance(ll[1:3], list) and len(ll[1:3]) == 2
+    assert len(ll[:0]) == 0 and len(ll[:-1]) == 4
+    with pytest.raises(IndexError):
+        v[3]
+    del v[2:]
+    assert len(v) == 2 and len(ll) == 5
+    assert v.pop()[0, 0, 0, 0] == 1 and len(v) == 1
+    with pytest.raises(TypeError):
+        del ll[1:3]
+    with pytest.raises(TypeError):
+        ll.pop(0)
+    del ll[4]
+    assert len(ll) == 4
