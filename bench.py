@@ -14,7 +14,7 @@ environment launches N ranks itself through torch.distributed.run before touchin
   c4     BASELINE configs[3]: one step is a batch of 64 independent pairs, rank r solves
          pairs r::N (strong scaling over the fixed batch; no collective);
   c5     one 4096^2 pair per step, its 256 tiles sharded over the ranks, results
-         all-gathered (RCCL over xGMI) and stitched (strong scaling).
+         gathered to rank 0 (RCCL over xGMI), which stitches (strong scaling).
 Timing is barrier + synchronize bracketed, max over ranks.  Consecutive pair solves are
 pipelined over 2 HIP streams (--streams): a solve's level kernel waits for the previous
 solve's level kernel, and the previous pair's latency-bound tail (levels >= 3, matching,
@@ -49,6 +49,8 @@ S = 128
 GRID = 8
 CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c4': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
 C4_PAIRS = 64                  # BASELINE configs[3]: a batch of 64 independent 1024^2 pairs
+BASELINE_LEVELS = {'c2': 3, 'c3': 4, 'c4': 4}   # BASELINE configs[1..3]: "3-level" / "4-level pyramid"
+SPEC_CLOCK_GHZ = 2.4           # MI355X_MICROARCH.md: max clock (the issue roofline's peak)
 # Rehearsal of the multi-rank path on a box with fewer GPUs than ranks (tests/test_bench_ranks.py):
 # DM_BENCH_BACKEND=gloo and DM_BENCH_ONE_DEVICE=1 put every rank on cuda:0 over gloo.  The
 # driver's runs leave both unset: one rank per GPU over RCCL ("nccl").
@@ -75,6 +77,15 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample-tiles', type=int, default=16)
     ap.add_argument('--no-volume', action='store_true')
+    ap.add_argument('--levels', type=int, default=None,
+                    help='k-level pyramid (BASELINE configs C2 "3-level", C3 "4-level"): build and match '
+                         'levels 0..k-1 only, as the reference Matching on co_map_list[:k] with '
+                         'N_map = 2^(k-1); default: the full pyramid Correlation_map builds')
+    ap.add_argument('--output-hash', action='store_true',
+                    help="after timing, solve once more and report sha256 of rank 0's stitched "
+                         "maps of its first pair (tests compare it across rank counts)")
+    ap.add_argument('--no-k-level', action='store_true',
+                    help='skip the extra timed pass at BASELINE\'s k-level pyramid')
     return ap.parse_args()
 
 
@@ -82,13 +93,15 @@ class PairSolver:
     """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
     dominant kernel (dm_corr_level12)."""
 
-    def __init__(self, img1, img2, tile, grid, split=False):
+    def __init__(self, img1, img2, tile, grid, split=False, levels=None):
         """split: the pair's tiles are sharded over the ranks (rank r solves tiles r::N) and
-        the per-tile results are all-gathered before stitching (RCCL over xGMI); otherwise
-        this rank solves every tile of its own pair."""
+        the per-tile results are gathered to rank 0 (RCCL over xGMI), which stitches the map;
+        otherwise this rank solves every tile of its own pair.  levels: k-level pyramid
+        (None: the full pyramid)."""
         from deepmatching_stereo_matching_amd import shard
         self.dev = img1.device
         self.tile = tile
+        self.levels = levels
         self.n, origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
         assert self.n == [grid, grid], self.n
         self.rank, self.world = shard.world() if split else (0, 1)
@@ -108,18 +121,24 @@ class PairSolver:
             with torch.cuda.stream(stream):
                 return self.step(timed=timed, wait=wait)
         from deepmatching_stereo_matching_amd import shard
+        match = self.compute(timed=timed, wait=wait)
+        if self.world > 1:   # rank 0 receives every tile's (3, S, S) result and stitches
+            match = shard.gather_units_to(match, self.T, self.rank, self.world, 0)
+            if match is None:
+                return None
+        return engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
+                             ['elevation'])
+
+    def compute(self, timed=False, wait=None):
+        """This rank's tiles: stats, dm_corr_level12 [timed], dm_aggregate levels 3.., matching
+        with sub-pixel -> float64 [T_rank][3][S][S] on the current stream."""
         pyr = engine.DevicePyramid(self.batch, build=False)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         if timed:
             self.ev.append(ev)
         self.last_end = ev[1]
-        pyr.build(events=ev, wait=wait)    # stats, dm_corr_level12 [timed], dm_aggregate levels 3..
-        match = pyr.match(sub_pix=True)
-        if self.world > 1:
-            match = shard._gather_units(match, self.T, self.rank, self.world, match.shape[1:], match.dtype)
-        dmap, score = engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
-                                    ['elevation'])
-        return dmap, score
+        pyr.build(events=ev, wait=wait, nlev=self.levels)
+        return pyr.match(sub_pix=True, nlev=self.levels)
 
     def level1_ms(self):
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
@@ -159,7 +178,7 @@ def volume_roofline(solver, reps=3, f16=False):
             'algorithmic_bytes_per_voxel': esz, 'bound': 'hbm',
             'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
-            'traffic': load_traffic(batch.h0, 'volume_f16' if f16 else 'volume')}
+            'traffic': load_traffic(batch.h0, 'volume_f16' if f16 else 'volume', batch.T)}
 
 
 def fp16_flip_rate(solver, tiles=2):
@@ -210,73 +229,112 @@ def cpu_baseline(tiles, tile):
                                            'repo cv2 shim, 8-core Xeon (SURVEY.md section 6)'}}
 
 
-def load_pmc(tile, kernel='level1'):
+def load_pmc(tile, kernel='level1', tiles=None):
     """Per-launch PMC figures of a kernel from the committed rocprofv3 passes
-    (profiles/pmc_<kernel>.json, tools/profile.sh): HBM bytes (FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE) and, for the level kernel, VALU instructions."""
-    path = os.path.join(REPO, 'profiles', 'pmc_%s.json' % kernel)
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get('tile') == tile:
+    (profiles/pmc_<kernel>.json for the C3 shape, pmc_<kernel>_s<tile>.json for others;
+    tools/profile.sh): HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) and, for the
+    level kernel, VALU instructions, the issue-cycle model and the clock.  Only a file made on
+    the same tile size (and, when given, the same tiles per launch) is used."""
+    for name in ('pmc_%s.json' % kernel, 'pmc_%s_s%d.json' % (kernel, tile)):
+        try:
+            with open(os.path.join(REPO, 'profiles', name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get('tile') == tile and (tiles is None or d.get('tiles', 64) == tiles):
             return d
-    except (OSError, ValueError):
-        pass
     return {}
 
 
-def load_traffic(tile, kernel='level1'):
-    return load_pmc(tile, kernel).get('hbm_bytes_per_launch')
+def load_traffic(tile, kernel='level1', tiles=None):
+    return load_pmc(tile, kernel, tiles).get('hbm_bytes_per_launch')
 
 
 def level_roofline(solver, tile, l1_ms):
     """Roofline of the dominant kernel, dm_corr_level12 (k_level1_mfq): levels 0 -> 1 -> 2 in
     one pass, level 0 and level 1 never leave the chip.
 
-    It is compute-bound: its physical HBM traffic (PMC, ~1.24 GB per C3 launch) is ~1.5 % of
-    what the bandwidth would allow in its run time.  The bound is the vector ALU (float32
-    normalisation, float64 pow14 of every pooled child value), so `achieved` / `peak` are
-    VALU-busy SIMD-cycles per second against 1024 SIMDs x the clock the kernel ran at, both
-    from a committed rocprofv3 --pmc pass (profiles/pmc_level1.json, tools/pmc_valu.sh):
-    SQ_ACTIVE_INST_VALU (quad-cycles) x 4 per launch over the live HIP-event time, and the
-    effective clock GRBM_GUI_ACTIVE / 8 XCDs / profiled kernel time.  The 4 B/voxel figure of
-    SURVEY.md 8(d) (the level-0 volume this kernel does not write) is kept as
-    `hbm_equivalent`."""
-    vox_launch = solver.batch.T * float(tile) ** 4   # this rank's tiles per launch
-    gbs = 4.0 * vox_launch / (l1_ms * 1e-3) / 1e9
+    It is bound by vector-instruction issue, not by HBM (its physical traffic, ~1.2 GB per C3
+    launch, is ~1.5 % of what the bandwidth allows in its run time) and not by the matrix
+    cores.  achieved = the launch's issue cycles / its LIVE time (HIP events around every timed
+    launch, on the launch stream); peak = 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md max clock).
+    The issue cycles per launch are a model (source 'profile'): the kernel's ISA, each
+    instruction priced by what tools/valu_probe.hip measured on gfx950 (2.2 cycles for the
+    simple VOP2/VOP1 32-bit ops, 4 for float64, packed float32, VOP3 and DPP forms, 8 for an
+    MFMA's hold on its SIMD), times how often each block runs (tools/isa_cost.py,
+    profiles/pmc_level1.json: the modelled instruction count is checked against the PMC
+    SQ_INSTS_VALU of the same build).  frac_at_profiled_clock uses the clock the chip held in
+    the committed PMC pass (GRBM_GUI_ACTIVE / 8 / kernel time) instead of 2.4 GHz.
+    valu_busy_pmc (SQ_ACTIVE_INST_VALU x 4 / (1024 x cycles)) prices every VALU instruction at
+    4 cycles: an upper bound, kept for comparison with round 2."""
     mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
     kname = ('dm_corr_level1 (k_level1_mfq)' if mode == 0
              else 'dm_corr_level12 (k_level1_mfq, level 2 fused)')
-    pmc = load_pmc(tile) if solver.batch.T == 64 else {}
-    roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3)}
-    busy, cyc = pmc.get('valu_active_cycles_per_launch'), pmc.get('gpu_cycles_per_launch')
-    if busy and cyc:
-        # the launch's cycle count is taken from the PMC pass (the kernel is deterministic); the
-        # live time then gives the clock it ran at in this run, so achieved / peak is the
-        # measured VALU-busy fraction
-        achieved = busy / (l1_ms * 1e-3) / 1e9          # G SIMD-cycles/s with the VALU busy
-        peak = 1024 * cyc / (l1_ms * 1e-3) / 1e9
-        roof.update({'achieved': round(achieved, 1), 'peak': round(peak, 1),
-                     'unit': 'G VALU-busy SIMD-cycles/s', 'frac': round(achieved / peak, 4),
-                     'valu_busy_source': 'SQ_ACTIVE_INST_VALU x4 (one quad-cycle per wave64 VALU '
-                                         'instruction) per launch over 1024 SIMDs x GRBM_GUI_ACTIVE/8 '
-                                         'cycles per launch, rocprofv3 --pmc (profiles/pmc_level1.json)'})
-        for k in ('ta_busy_frac', 'td_busy_frac'):
-            if k in pmc:
-                roof[k] = pmc[k]
+    pmc = load_pmc(tile, 'level1', solver.batch.T)
+    peak = 1024 * SPEC_CLOCK_GHZ
+    roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3),
+            'unit': 'G SIMD-issue-cycles/s', 'peak': peak}
+    cyc = pmc.get('issue_cycles_per_launch')
+    if cyc:
+        achieved = cyc / (l1_ms * 1e-3) / 1e9
+        roof.update({'achieved': round(achieved, 1), 'frac': round(achieved / peak, 4)})
+        if pmc.get('clock_ghz'):
+            roof['frac_at_profiled_clock'] = round(achieved / (1024 * pmc['clock_ghz']), 4)
+            roof['profiled_clock_ghz'] = pmc['clock_ghz']
+        roof['source'] = {'time': 'live: HIP events around every timed launch on its stream',
+                          'issue_cycles_per_launch': 'profile: ' + pmc.get('issue_model_note', ''),
+                          'peak': '1024 SIMDs x 2.4 GHz, MI355X_MICROARCH.md'}
     else:
-        roof.update({'achieved': None, 'peak': None, 'unit': 'G VALU-busy SIMD-cycles/s',
-                     'frac': None, 'valu_busy_source': 'no PMC pass for this batch shape'})
-    if pmc.get('valu_insts_per_launch'):
-        # issue-limited estimate: a wave64 VALU instruction occupies a 32-lane SIMD >= 2 cycles
-        roof['valu_insts_per_launch'] = pmc['valu_insts_per_launch']
-    roof['traffic'] = load_traffic(tile) if pmc else None
-    roof['hbm_equivalent'] = {'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                              'frac': round(gbs / HBM_PEAK_GBS, 4),
-                              'algorithmic': '4 B/voxel x %d level-0 voxels per launch (never '
-                                             'written: the volume a materialising kernel would '
-                                             'store)' % int(vox_launch)}
+        roof.update({'achieved': None, 'frac': None,
+                     'source': {'issue_cycles_per_launch': 'no issue model for this batch shape'}})
+    if pmc.get('valu_busy_frac'):
+        roof['valu_busy_pmc'] = {'value': pmc['valu_busy_frac'], 'source': 'profile',
+                                 'note': 'SQ_ACTIVE_INST_VALU x 4 over 1024 SIMDs x GRBM cycles: '
+                                         'every VALU instruction priced at 4 cycles (upper bound)'}
+    for k in ('valu_insts_per_launch', 'ta_busy_frac', 'td_busy_frac'):
+        if k in pmc:
+            roof[k] = pmc[k]
+    roof['traffic'] = pmc.get('hbm_bytes_per_launch')
     return roof
+
+
+def volume_equivalent(solver, tile, l1_ms):
+    """NOT a roofline: the rate at which the fused level kernel consumes level-0 voxels,
+    expressed as the HBM bandwidth a kernel that wrote the float32 volume (4 B
+    per voxel) would need.  It can exceed the 8 TB/s peak because this kernel never writes
+    the volume."""
+    vox = solver.batch.T * float(tile) ** 4
+    gbs = 4.0 * vox / (l1_ms * 1e-3) / 1e9
+    return {'gb_s': round(gbs, 1), 'vs_hbm_peak': round(gbs / HBM_PEAK_GBS, 4),
+            'voxels_per_launch': int(vox),
+            'note': 'level-0 voxels per launch x 4 B / live kernel time; the volume is never written'}
+
+
+def split_breakdown(solver, rank, world, dev):
+    """c5 split: one more (untimed) solve, instrumented per rank -- compute (this rank's tiles:
+    pyramid + matching), gather to rank 0, stitch (rank 0) -- in ms, for every rank."""
+    import torch.distributed as tdist
+    from deepmatching_stereo_matching_amd import shard
+    torch.cuda.synchronize()
+    tdist.barrier()
+    t0 = time.perf_counter()
+    match = solver.compute()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    full = shard.gather_units_to(match, solver.T, rank, world, 0)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if full is not None:
+        engine.stitch(full, solver.n, solver.tile, solver.tile, [solver.tile, solver.tile], ['elevation'])
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    mine = torch.tensor([t1 - t0, t2 - t1, t3 - t2, float(len(solver.origins))], dtype=torch.float64,
+                        device=dev if BACKEND == 'nccl' else 'cpu')
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    tdist.all_gather(parts, mine)
+    return [{'rank': r, 'tiles': int(p[3]), 'compute_ms': round(float(p[0]) * 1e3, 3),
+             'gather_ms': round(float(p[1]) * 1e3, 3), 'stitch_ms': round(float(p[2]) * 1e3, 3)}
+            for r, p in enumerate(parts)]
 
 
 def launch_ranks(args):
@@ -356,7 +414,7 @@ def main():
     solvers = []
     for a, b in host_pairs:
         img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
-        solvers.append(PairSolver(img1, img2, tile, grid, split=split))
+        solvers.append(PairSolver(img1, img2, tile, grid, split=split, levels=args.levels))
     del host_pairs
     solver = solvers[0] if solvers else None
     voxels = grid * grid * float(tile) ** 4      # per pair
@@ -365,10 +423,11 @@ def main():
     # solve's level kernel waits for the previous solve's level kernel (so level kernels never
     # share the GPU with each other and each one's event time stays its own), while the
     # previous pair's latency-bound tail (levels >= 3, matching on demand, stitch: ~5 % of a
-    # solve) runs beside it.  Each solve still solves its pair completely.
-    # c5 split over ranks all-gathers inside every solve: its collectives stay on one stream
-    # (RCCL operations of one communicator must not race each other on two streams)
-    nstreams = 1 if split else max(1, args.streams)
+    # solve) runs beside it.  Each solve still solves its pair completely.  The c5 split's
+    # gather to rank 0 is issued from whichever stream the solve runs on: one process group's
+    # collectives run in issue order on its own communication stream, each waiting for the
+    # issuing stream, so solves on two streams gather in order.
+    nstreams = max(1, args.streams)
     streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)] if nstreams > 1 else [None]
     nsolve = [0]
     prev_end = [None]
@@ -380,56 +439,103 @@ def main():
             s.step(timed=timed, stream=st, wait=prev_end[0] if st is not None else None)
             prev_end[0] = s.last_end
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def run(steps, warmup, timed=True):
+        """warmup untimed steps, then `steps` timed ones bracketed by barrier + synchronize;
+        seconds, max over ranks"""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(timed=timed)
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
+    elapsed = run(args.steps, args.warmup)
     ms_step = elapsed / args.steps * 1e3
     value = job_pairs * args.steps * voxels / elapsed / 1e9
     l1_ms = solver.level1_ms() if solver else None
     if rank == 0 and solver is None:
         raise SystemExit('rank 0 has no pairs (--pairs < --gpus)')
+
+    # BASELINE.json states C2 / C3 (/ C4) on a 3- / 4-level pyramid: the same timed run with
+    # the pyramid cut to k levels (levels 0..k-1 built, matching starts at level k-1), next to
+    # the full pyramid Correlation_map always builds
+    k_level = None
+    k = BASELINE_LEVELS.get(args.config)
+    if args.levels is None and k and not args.no_k_level and not split:
+        for s_ in solvers:
+            s_.levels = k
+        el_k = run(args.steps, 1, timed=False)
+        for s_ in solvers:
+            s_.levels = None
+        k_level = {'levels': k, 'ms_per_step': round(el_k / args.steps * 1e3, 3),
+                   'ms_per_pair': round(el_k / args.steps * 1e3 / job_pairs, 3),
+                   'value': round(job_pairs * args.steps * voxels / el_k / 1e9, 3), 'unit': 'Gvox/s',
+                   'note': 'same workload and timing, pyramid cut to %d levels (co_map_list[:%d], '
+                           'N_map = %d)' % (k, k, 2 ** (k - 1))}
+
+    breakdown = split_breakdown(solver, rank, world, dev) if split else None
+    out_hash = None
+    if args.output_hash:
+        import hashlib
+        res = solvers[0].step() if solvers else None    # split: every rank takes part
+        torch.cuda.synchronize()
+        if res is not None:
+            h = hashlib.sha256()
+            for t in res:
+                h.update(t.cpu().numpy().tobytes())
+            out_hash = h.hexdigest()
+
     if rank == 0:
         roof = level_roofline(solver, tile, l1_ms)
+        lv = ('%d-level pyramid' % args.levels) if args.levels else 'full pyramid'
         if args.config == 'c4':
             workload = ('C4: batch of %d independent %dx%d pairs per step (%dx%d tiles of S=%d each), '
-                        'ws=%d, full pyramid + sub-pixel + cal_map + stitch'
-                        % (job_pairs, grid * tile, grid * tile, grid, grid, tile, WS))
+                        'ws=%d, %s + sub-pixel + cal_map + stitch'
+                        % (job_pairs, grid * tile, grid * tile, grid, grid, tile, WS, lv))
             per_gpu, par = job_pairs / float(world), 'pairs of the batch sharded %d-way' % world
         else:
-            workload = ('%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, full pyramid '
+            workload = ('%s: %dx%d pair, %dx%d tiles of S=%d, ws=%d, %s '
                         '+ sub-pixel + cal_map + stitch'
-                        % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS))
+                        % (args.config.upper(), grid * tile, grid * tile, grid, grid, tile, WS, lv))
             per_gpu = (1.0 / world) if split else 1
-            par = ('tiles of one pair sharded %d-way' if split else 'pairs sharded %d-way') % world
+            par = ('tiles of one pair sharded %d-way, gathered to rank 0' if split
+                   else 'pairs sharded %d-way') % world
         rec = {'metric': 'correlation-volume G-voxels/sec + ms/stereo-pair @1/8 GPU, 1024^2 d=128',
                'value': round(value, 3), 'unit': 'Gvox/s', 'n_gpus': joined, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),
-               'ms_per_pair': round(ms_step / job_pairs * world, 3),
+               # wall time per pair of the whole job, and GPU time per pair (ms_step x GPUs / pairs)
+               'ms_per_pair': round(ms_step / job_pairs, 3),
+               'gpu_ms_per_pair': round(ms_step / job_pairs * world, 3),
                'higher_is_better': True,
                'scaling': 'strong' if (split or args.config == 'c4') else 'weak',
                'vs_baseline': None, 'dtype': 'u8->i32/f32/f64',
                'data': 'synthetic (Gaussian-smoothed uniform texture, sinusoidal shift)',
                'config': {'workload': workload, 'tile': tile, 'tiles_per_pair': grid * grid,
-                          'window_size': WS, 'pairs_per_step': job_pairs,
+                          'window_size': WS, 'pyramid_levels': args.levels or 'full',
+                          'pairs_per_step': job_pairs,
                           'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
                           'streams': nstreams},
-               'roofline': roof}
+               'roofline': roof,
+               'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
+        if k_level:
+            rec['k_level'] = k_level
+        if out_hash:
+            rec['output_sha256'] = out_hash
+        if breakdown:
+            rec['split_breakdown'] = breakdown
         if not args.no_volume:
             rec['volume_kernel_roofline'] = volume_roofline(solver)
             rec['volume_f16_kernel_roofline'] = volume_roofline(solver, f16=True)

@@ -129,13 +129,37 @@ __device__ __forceinline__ double pow14_q4(double s, const PowLds &t)
 // NaN -> NaN (the g32 NaN row).  Fewer integer ops than pow14_zd: exponent, index and
 // mantissa come straight from the f32 bits, and r = M c_i - 1 is exact in float32 (24-bit M,
 // 10-bit c_i, |r| < 2^-9), so one float32 FMA forms the float64 FMA's value.
-__device__ __forceinline__ double pow14_zf(float x, const PowLds &t)
+// The LDS byte offsets come straight from the f32 bits, two VOP2 ops each (2.2 issue cycles
+// apiece, tools/valu_probe.hip) instead of a bfe, a shift and a mad_u32_u24 (4 + 2.2 + 4):
+// fp row i (16 B) at (u >> 10) & 0x1FF0, fc32[i] at a quarter of that, g32 row be at
+// (u >> 19) & 0xFF0.
+// M = (u & 0x7FFFFF) | 1.0f as v_bitop3_b32 (2.1 issue cycles) instead of v_and_or_b32 (4);
+// `mant` is 0x7FFFFF in a VGPR (an SGPR operand costs the VOP3 forms 4 cycles).
+static_assert(DM_POWF_NT == 512, "pow14_zf's offsets assume 9 mantissa index bits");
+__device__ __forceinline__ unsigned mant_mask_vgpr()
+{
+    unsigned m;
+    asm volatile("v_mov_b32 %0, 0x7fffff" : "=v"(m));
+    return m;
+}
+__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)
 {
     const unsigned u = __float_as_uint(x);
-    const float M = __uint_as_float((u & 0x7FFFFFu) | 0x3F800000u);
-    const int i = (int)((u >> 14) & (DM_POWF_NT - 1));
-    const int be = (int)((u >> 23) & 0xFF);
-    return pow14_core_r((double)__builtin_fmaf(M, t.fc32[i], -1.0f), i, t.g32[be], t);
+    // bitop3 truth table 0xEA = (src0 & src1) | src2
+    const float M = __uint_as_float(__builtin_amdgcn_bitop3_b32(u, mant, 0x3F800000u, 0xEA));
+    const unsigned ofp = (u >> 10) & 0x1FF0u, og = (u >> 19) & 0xFF0u;
+    const float ci = *(const float *)((const char *)t.fc32 + (ofp >> 2));
+    const dm_d2 G = *(const dm_d2 *)((const char *)t.g32 + og);
+    const dm_d2 Pr = *(const dm_d2 *)((const char *)t.fp + ofp);
+    const double r = (double)__builtin_fmaf(M, ci, -1.0f);
+    double q = DM_POWF_B5;
+    q = fma(q, r, DM_POWF_B4);
+    q = fma(q, r, DM_POWF_B3);
+    q = fma(q, r, DM_POWF_B2);
+    q = fma(q, r, DM_POWF_B1);
+    q = fma(q, r, G.y);
+    const double s = fma(Pr.x, q, Pr.y) * G.x;
+    return fma(Pr.x, G.x, s);
 }
 
 __device__ __forceinline__ double pow14_lds(double x, const PowLds &t)

@@ -440,7 +440,22 @@ __global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const
 // min/max is reduced over the waves through LDS once; MaxPool's left neighbour of column
 // group w (q1 = 16*GW*w - 1) comes from wave w-1 through LDS once per image row.
 // ===================================================================================
-__device__ __forceinline__ double nanmax_d(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
+// MaxPool of one level-1 CELL's map: a plain IEEE max (v_max_f64) is torch's NaN-propagating
+// MaxPool here, because a cell's level-1 map is all-NaN or NaN-free.  x = (r - rmin) / den is
+// NaN only for den == 0 (a constant child map: a = 0 and rinv = inf, for EVERY window), and
+// every level-1 value of the cell sums all four children, so one such child makes every value
+// of the cell NaN and otherwise none is (y, r, x, pow14 are finite).  Every operand of these
+// maxima belongs to one cell (the lane group; the edge value of wave w-1 is the same cell), so
+// they are all NaN (max = NaN) or all finite.  Out-of-range neighbours (padding) are replaced by
+// the value itself instead of -inf, which keeps a NaN cell NaN.  (A NaN-aware max -- two
+// float64 compares and two selects, 16 issue cycles -- becomes one 4-cycle instruction.)
+// (inline asm: llvm.maxnum would add a canonicalising v_max_f64 x, x per operand)
+__device__ __forceinline__ double cellmax_d(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS byte address m0 + 16 * lane;
 // m0 is saved and restored around it (the compiler owns m0)
@@ -502,6 +517,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     }
     const int ab = YF ? DM_YBIAS : 0;
     const dm_v4i acc0 = {ab, ab, ab, ab};
+    const unsigned mant = mant_mask_vgpr();   // pow14_zf's mantissa mask, kept in a VGPR
     const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
     const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
 
@@ -628,19 +644,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     // of one per level-1 value.
     auto level2_row = [&](int u, const double (&l1p)[M]) {
         const double lft = __shfl(l1p[M - 1], lane - 1);
-        const double left = c != 0 ? lft : (wave == 0 ? -INFINITY : xch2[u & 1][wave - 1][grp]);
+        // column -1 is padding: the value itself stands in (cellmax_d)
+        const double left = c != 0 ? lft : (wave == 0 ? l1p[0] : xch2[u & 1][wave - 1][grp]);
         double Cq[M2];
         if constexpr (M == 1) { // L2 column 4*GW*w + c/2 on even lanes
             const double right = __shfl(l1p[0], lane + 1);
-            Cq[0] = nanmax_d(nanmax_d(left, l1p[0]), right);
+            Cq[0] = cellmax_d(cellmax_d(left, l1p[0]), right);
         } else {
 #pragma unroll
             for (int j = 0; j < M2; ++j)
-                Cq[j] = nanmax_d(nanmax_d(j == 0 ? left : l1p[2 * j - 1], l1p[2 * j]), l1p[2 * j + 1]);
+                Cq[j] = cellmax_d(cellmax_d(j == 0 ? left : l1p[2 * j - 1], l1p[2 * j]), l1p[2 * j + 1]);
         }
         if ((u & 1) == 0) {
 #pragma unroll
-            for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : nanmax_d(Cprev2[j], Cq[j]);
+            for (int j = 0; j < M2; ++j) Racc2[j] = u == 0 ? Cq[j] : cellmax_d(Cprev2[j], Cq[j]);
         } else {
             // the wave's 4*GW level-2 values of row u2 (cell sums on lanes of group 0) go to
             // the LDS stash; every L2B rows one pow per lane rectifies them all
@@ -648,7 +665,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             if constexpr (M == 1) {
                 // even lanes hold the pooled children: collect RB rows, rectify all 64 entries
                 // with one pow per lane, then sum the children (ul, ur, ll, lr) per column
-                const double R2 = nanmax_d(Racc2[0], Cq[0]);
+                const double R2 = cellmax_d(Racc2[0], Cq[0]);
                 Cprev2[0] = Cq[0];
                 const int rb = u2 % RB;
                 if ((c & 1) == 0) stash2[wave][rb * 4 * L2V + grp * L2V + c / 2] = R2;
@@ -672,7 +689,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             } else {
 #pragma unroll
                 for (int j = 0; j < M2; ++j) {
-                    const double R2 = pow14_q4(nanmax_d(Racc2[j], Cq[j]), plds); // pooled child, rectified
+                    const double R2 = pow14_q4(cellmax_d(Racc2[j], Cq[j]), plds); // pooled child, rectified
                     Cprev2[j] = Cq[j];
                     const double s0 = __shfl(R2, c), s1 = __shfl(R2, c + 16), s2 = __shfl(R2, c + 32),
                                  s3 = __shfl(R2, c + 48);
@@ -759,7 +776,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             double sum = 0.0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
-                const double pv = pow14_zf(x[r], plds);
+                const double pv = pow14_zf(x[r], plds, mant);
                 sum = r == 0 ? pv : sum + pv;
             }
             // level 1 = pow14(sum / 4), rectified where it is read: here when level 1 is
@@ -998,6 +1015,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
     }
     const int ab = YF ? DM_YBIAS : 0;
     const dm_v4i acc0 = {ab, ab, ab, ab};
+    const unsigned mant = mant_mask_vgpr();   // pow14_zf's mantissa mask, kept in a VGPR
     const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
     const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void *)Bt, 0, 0x7fffffff, 0x00020000);

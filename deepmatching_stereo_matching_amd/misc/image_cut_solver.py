@@ -110,10 +110,11 @@ class ImageCutSolver():
 
     def _execute_matching_device(self):
         """All tiles in batches on the GPU -> (d_map, out_map) device tensors.  The tile grid
-        is self.len, counted on the image shape BEFORE _padding (:46,58-62).  With a
-        torch.distributed process group initialised, the tiles are sharded over its ranks
-        (shard.solve_tiles_sharded: rank r solves tiles r::N, results all-gathered) and every
-        rank stitches the whole map."""
+        is self.len, counted on the image shape BEFORE _padding (:46,58-62).  Opted in to tile
+        sharding (shard.tile_sharding() or DM_SHARD_TILES=1) under a torch.distributed process
+        group, the tiles are sharded over its ranks (shard.solve_tiles_sharded: rank r solves
+        tiles r::N, results all-gathered) and every rank stitches the whole map; every rank
+        must then solve the same pair."""
         from deepmatching_stereo_matching_amd import shard
         n = list(self.len)
         if n[0] < 1 or n[1] < 1:
@@ -125,7 +126,7 @@ class ImageCutSolver():
         args = (self.img1, self.img2, origins, h0, w0, self.window_size,
                 L.METHODS[self.feature_name], self.sub_pix, self.filtering,
                 self.filtering_window_size, self.filtering_num, self.filtering_mode)
-        if shard.world()[1] > 1:
+        if shard.tile_sharding_enabled():
             match = shard.solve_tiles_sharded(*args)
         else:
             match = engine.solve_tiles(*args)

@@ -8,11 +8,19 @@ CPU in the tests).  Every rank holds the whole input image (read from disk or br
 once), so a tiled pair needs no halo exchange.
 """
 
+import contextlib
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import engine
+
+# Tile sharding of the mirror ImageCutSolver is OPT-IN: a process group alone does not turn it
+# on (ranks that each solve their own pairs, solve_pairs_sharded, must not enter one
+# collective per pair).  None: the DM_SHARD_TILES environment variable decides (1 = on).
+_TILE_SHARDING = None
 
 
 def world():
@@ -20,6 +28,28 @@ def world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+@contextlib.contextmanager
+def tile_sharding(enabled=True):
+    """Inside this block, ImageCutSolver()() (misc/image_cut_solver.py) shards its tiles over
+    the process group: every rank must then call it with the SAME pair, and collectively
+    (rank r solves tiles r::N, results gathered to every rank).  tile_sharding(False) turns it
+    off whatever DM_SHARD_TILES says."""
+    global _TILE_SHARDING
+    prev = _TILE_SHARDING
+    _TILE_SHARDING = bool(enabled)
+    try:
+        yield
+    finally:
+        _TILE_SHARDING = prev
+
+
+def tile_sharding_enabled():
+    """True when ImageCutSolver should shard its tiles: opted in (tile_sharding() or
+    DM_SHARD_TILES=1) and a process group of more than one rank is initialised."""
+    on = _TILE_SHARDING if _TILE_SHARDING is not None else os.environ.get('DM_SHARD_TILES') == '1'
+    return bool(on) and world()[1] > 1
 
 
 def rank_units(n, rank, size):
@@ -47,6 +77,36 @@ def _gather_units(local, n, rank, size, shape, dtype):
         idx = rank_units(n, r, size)
         if idx:
             out[idx] = parts[r][:len(idx)]
+    return out.to(dev) if host else out
+
+
+def gather_units_to(local, n, rank, size, dst=0):
+    """Gather per-rank unit results ([k_r][*shape], units r::N) to rank ``dst`` only, in unit
+    order [n][*shape]; the other ranks get None.  Only the rank that stitches receives the
+    tiles: with nccl (RCCL over xGMI) each peer sends its k_r units device to device, one link
+    per peer, instead of every rank receiving every unit (all-gather).  gloo gathers host
+    copies; the result goes back to ``local``'s device."""
+    shape, dtype = tuple(local.shape[1:]), local.dtype
+    per = (n + size - 1) // size
+    host = size > 1 and local.is_cuda and dist.get_backend() == 'gloo'
+    dev = local.device
+    if len(local) == per and not host:
+        buf = local.contiguous()
+    else:
+        buf = torch.zeros((per,) + shape, dtype=dtype, device='cpu' if host else dev)
+        if len(local):
+            buf[:len(local)] = local
+    if size == 1:
+        return buf[:n]
+    parts = [torch.empty_like(buf) for _ in range(size)] if rank == dst else None
+    dist.gather(buf, parts, dst=dst)
+    if rank != dst:
+        return None
+    out = torch.empty((n,) + shape, dtype=dtype, device=buf.device)
+    for r in range(size):
+        k = len(rank_units(n, r, size))
+        if k:
+            out[r::size] = parts[r][:k]
     return out.to(dev) if host else out
 
 
@@ -84,6 +144,9 @@ def solve_image_sharded(img1, img2, image_size, stride, window_size, method, mod
 
 def solve_pairs_sharded(pairs, fn):
     """Independent pairs (BASELINE configs[3]): rank r runs fn(pair) for pairs r::N and
-    returns {pair index: result} for its own pairs (per-rank outputs, no collective)."""
+    returns {pair index: result} for its own pairs (per-rank outputs, no collective).  Ranks
+    hold different pairs (and different counts of them), so tile sharding is off inside fn:
+    an ImageCutSolver there solves its whole pair on this rank."""
     rank, size = world()
-    return {i: fn(pairs[i]) for i in rank_units(len(pairs), rank, size)}
+    with tile_sharding(False):
+        return {i: fn(pairs[i]) for i in rank_units(len(pairs), rank, size)}

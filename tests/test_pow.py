@@ -90,3 +90,71 @@ def test_fast_table_makes_float32_r_exact():
         i = int(u) >> 14
         exact = Fraction(M) * Fraction(cs[i]) - 1
         assert float(np.float32(float(exact))) == exact   # representable in float32
+
+
+def _pow14_array(x):
+    """The pinned pow on an array (oracle dmo_rectify_f64 in pinned mode)."""
+    y = np.ascontiguousarray(x, dtype=np.float64).copy()
+    O.set_pow_mode('pinned')
+    try:
+        O.lib().dmo_rectify_f64(y.ctypes.data_as(O.ctypes.c_void_p), y.size, O.LAM)
+    finally:
+        O.set_pow_mode('libm')
+    return y
+
+
+def test_pinned_pow_is_monotone():
+    """The level kernel pools BEFORE rectifying (MaxPool of pow14(s/4) == pow14 of the MaxPool,
+    dm_mfma.h level2_row; the sweeps pool y before r, x, pow14): that is bit-exact only if the
+    pinned pow is non-decreasing on adjacent doubles.  Checked where it can break -- both ends
+    of every one of the 512 mantissa bins (the c_i table edges) at every exponent of the fast
+    path [2^EMIN, 1], plus random points and their successors."""
+    emin = -319
+    i = np.arange(512, dtype=np.float64)
+    lo = 1.0 + i / 512.0                       # first double of bin i
+    hi = np.nextafter(1.0 + (i + 1) / 512.0, 0)  # last double of bin i
+    xs = []
+    for e in range(emin, 1):
+        s = np.ldexp(1.0, e)
+        for b in (lo, hi):
+            v = b * s
+            xs.append(np.nextafter(v, 0))
+            xs.append(v)
+            xs.append(np.nextafter(v, np.inf))
+    rng = np.random.default_rng(11)
+    r = np.exp2(rng.uniform(emin, 0, 200000))
+    x = np.concatenate(xs + [r])
+    x = x[(x > 0) & (x <= 1.0)]
+    nxt = np.minimum(np.nextafter(x, np.inf), 1.0)
+    a, b = _pow14_array(x), _pow14_array(nxt)
+    assert np.all(b >= a)
+    # and the ends of each bin meet the next bin's start without a step down
+    starts = np.concatenate([np.ldexp(lo, e) for e in range(emin, 0)])
+    prev = np.nextafter(starts, 0)
+    assert np.all(_pow14_array(starts) >= _pow14_array(prev))
+
+
+def test_pow_pin_vs_libm_within_bound():
+    """DESIGN.md section 2 / tools/pow_pin.py (profiles/pow_pin.json: 8 C3 tiles + 1 C5 tile,
+    0 of 196,608 correspondences flipped, levels within 7.5e-16 relative, sub-pixel within
+    1.5e-14): the kernels' pinned pow14 against libm (numpy's pow, the reference's) on one
+    S=32 tile of the same generator -- no integer correspondence moves, float64 levels and
+    sub-pixel values move by rounding only."""
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(36, 36, seed=1000, dx=2, max_disp=8, sinusoidal=True)
+    res = {}
+    for mode in ('libm', 'pinned'):
+        O.set_pow_mode(mode)
+        try:
+            lev, _, _ = O.pyramid_stream(a, b, 5)
+            res[mode] = (lev, O.match_stream(a, b, 5, lev, sub_pix=False),
+                         O.match_stream(a, b, 5, lev, sub_pix=True))
+        finally:
+            O.set_pow_mode('libm')
+    (l0, m0, s0), (l1, m1, s1) = res['libm'], res['pinned']
+    assert np.array_equal(m0[:2], m1[:2])
+    for x, y in zip(l0[1:], l1[1:]):
+        assert np.array_equal(np.isnan(x), np.isnan(y))
+        ok = ~np.isnan(x) & (x != 0)
+        assert np.max(np.abs(x[ok] - y[ok]) / np.abs(x[ok])) <= 4e-15
+    assert np.nanmax(np.abs(s0 - s1)) <= 1e-12

@@ -96,3 +96,82 @@ def test_sharded_image_equals_serial(size):
 def test_pairs_sharded_single_process():
     got = shard.solve_pairs_sharded(list(range(5)), lambda x: x * x)
     assert got == {i: i * i for i in range(5)}
+
+
+def _pairs_worker(rank, size, port, q):
+    """solve_pairs_sharded with the mirror ImageCutSolver inside fn and unequal pair counts
+    per rank (5 pairs over 3 ranks: 2/2/1), DM_SHARD_TILES=1 set: tile sharding must stay
+    off inside fn, so no rank enters a collective its peers do not (it used to
+    mix tiles of different pairs, or hang)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), DM_SHARD_TILES='1')
+    dist.init_process_group('gloo', rank=rank, world_size=size)
+    try:
+        _patch_engine()
+        from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+        pairs = _pairs()
+        got = shard.solve_pairs_sharded(
+            pairs, lambda p: ImageCutSolver(p[0], p[1], image_size=[16, 16], stride=[16, 16],
+                                            window_size=5)())
+        # and opted in explicitly with the SAME pair on every rank: tiles sharded, all-gathered
+        with shard.tile_sharding():
+            one = ImageCutSolver(pairs[0][0], pairs[0][1], image_size=[16, 16], stride=[16, 16],
+                                 window_size=5)()
+        q.put((rank, sorted(got), [got[i] for i in sorted(got)], one))
+    finally:
+        dist.destroy_process_group()
+
+
+def _pairs():
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    return [stereo_pair(16 * 2 + 4 + 16, 16 * 2 + 4 + 16, seed=30 + i, dx=1 + i % 2) for i in range(5)]
+
+
+def _patch_engine():
+    """The CPU stand-ins for the GPU solver and stitcher, returning torch tensors."""
+    def stitch(match, n, h0, w0, stride, modes):
+        d, s = _host_stitch(match, n, h0, w0, stride, modes)
+        return torch.from_numpy(d), torch.from_numpy(s)
+    engine.solve_tiles = _oracle_tiles
+    engine.stitch = stitch
+
+
+def test_pairs_sharded_with_image_cut_solver_unequal_counts():
+    ref_engine = (engine.solve_tiles, engine.stitch)
+    try:
+        _patch_engine()
+        from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+        ref = [ImageCutSolver(a, b, image_size=[16, 16], stride=[16, 16], window_size=5)()
+               for a, b in _pairs()]
+    finally:
+        engine.solve_tiles, engine.stitch = ref_engine
+    size = 3
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pairs_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(size)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = []
+    for rank, idx, outs, one in res:
+        assert idx == shard.rank_units(5, rank, size)
+        seen += idx
+        for i, (d, s) in zip(idx, outs):
+            assert np.array_equal(d, ref[i][0], equal_nan=True) and np.array_equal(s, ref[i][1], equal_nan=True)
+        assert np.array_equal(one[0], ref[0][0], equal_nan=True)
+        assert np.array_equal(one[1], ref[0][1], equal_nan=True)
+    assert sorted(seen) == list(range(5))
+
+
+def test_tile_sharding_is_opt_in(monkeypatch):
+    monkeypatch.delenv('DM_SHARD_TILES', raising=False)
+    assert not shard.tile_sharding_enabled()          # no process group, not opted in
+    with shard.tile_sharding():
+        assert not shard.tile_sharding_enabled()      # opted in, but a single process
+        with shard.tile_sharding(False):
+            assert shard._TILE_SHARDING is False
+        assert shard._TILE_SHARDING is True
+    assert shard._TILE_SHARDING is None

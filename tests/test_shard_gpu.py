@@ -38,7 +38,8 @@ def _worker(rank, size, port, q):
         d, s = shard.solve_image_sharded(a, b, [S, S], STRIDE, WS, 5, MODES)
         cut = ImageCutSolver(a, b, image_size=[S, S], stride=STRIDE, window_size=WS,
                              degree_map_mode=list(MODES))
-        d2, s2 = cut()
+        with shard.tile_sharding():      # opt-in: every rank solves this same pair together
+            d2, s2 = cut()
         dist.barrier()
         q.put((rank, d.cpu().numpy(), s.cpu().numpy(), d2, s2))
     except BaseException as e:   # report, do not hang the parent
