@@ -157,28 +157,43 @@ def volume_roofline(solver, reps=3, f16=False):
     pyr.compute_stats()
     vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float16 if f16 else torch.float32,
                       device=batch.device)
-    fn = pyr.lib.dm_corr_volume_f16 if f16 else pyr.lib.dm_corr_volume
-    ts = []
-    for i in range(reps + 1):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        L.check(fn(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
-        e1.record()
-        torch.cuda.synchronize()
-        if i:
-            ts.append(e0.elapsed_time(e1))
-    ms = float(np.mean(ts))
     voxels = batch.T * batch.P * batch.P
-    gbs = esz * voxels / (ms * 1e-3) / 1e9
+
+    def timed(flags):
+        ts = []
+        for i in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(pyr.lib.dm_corr_volume_ex(batch.ref(), L.ptr(pyr.stats), flags, L.ptr(vol),
+                                              L.stream_handle()))
+            e1.record()
+            torch.cuda.synchronize()
+            if i:
+                ts.append(e0.elapsed_time(e1))
+        ms = float(np.mean(ts))
+        gbs = esz * voxels / (ms * 1e-3) / 1e9
+        return ms, gbs
+
+    f = L.DM_VOLUME_F16 if f16 else 0
+    ms, gbs = timed(f)          # standalone: computes the per-patch min/max itself
+    ms_k, gbs_k = timed(f | L.DM_VOLUME_MINMAX_KNOWN)
     del vol, pyr
     torch.cuda.empty_cache()
     name = 'dm_corr_volume_f16 (k_volume_ls, binary16)' if f16 else 'dm_corr_volume (k_volume_ls)'
+    key = 'volume_f16' if f16 else 'volume'
     return {'kernel': name, 'tiles': batch.T, 'tile': batch.h0,
             'ms': round(ms, 3), 'gvox_s': round(voxels / (ms * 1e-3) / 1e9, 1),
             'algorithmic_bytes_per_voxel': esz, 'bound': 'hbm',
             'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
-            'traffic': load_traffic(batch.h0, 'volume_f16' if f16 else 'volume', batch.T)}
+            'traffic': load_traffic(batch.h0, key, batch.T),
+            'minmax_known': {
+                'what': 'the same volume, per-patch min/max already in the stats workspace (after '
+                        'the level kernel, as Correlation_map()() then co_map): dm_corr_volume_ex '
+                        'with DM_VOLUME_MINMAX_KNOWN skips the min/max sweep',
+                'ms': round(ms_k, 3), 'achieved': round(gbs_k, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(gbs_k / HBM_PEAK_GBS, 4),
+                'traffic': load_traffic(batch.h0, key + '_mm', batch.T)}}
 
 
 def fp16_flip_rate(solver, tiles=2):

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get('DM_LIB_PATH') or os.path.join(HERE, 'libdmstereo.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'dmstereo.h')
 
 DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3, -4
+DM_VOLUME_F16, DM_VOLUME_MINMAX_KNOWN = 1, 2   # dm_corr_volume_ex flags
 DM_TM_CCOEFF, DM_TM_CCOEFF_NORMED = 4, 5
 METHODS = {'cv2.TM_CCOEFF_NORMED': DM_TM_CCOEFF_NORMED, 'cv2.TM_CCOEFF': DM_TM_CCOEFF}
 CAL_MODES = {'elevation': 0, 'elevation2': 1, 'distance': 2}
@@ -53,6 +54,7 @@ SIGNATURES = {
     'dm_corr_level12': ([_TP, _P, _P, _P, _P], ctypes.c_int),
     'dm_corr_volume': ([_TP, _P, _P, _P], ctypes.c_int),
     'dm_corr_volume_f16': ([_TP, _P, _P, _P], ctypes.c_int),
+    'dm_corr_volume_ex': ([_TP, _P, _I, _P, _P], ctypes.c_int),
     'dm_rectify_f16': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify64': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),

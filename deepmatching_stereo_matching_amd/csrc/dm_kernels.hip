@@ -1326,7 +1326,8 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 // i8 operands); DM_VOLUME_IMPL=cs selects the column-split kernel (A/B), DM_VOLUME_LSNW=8
 // eight waves (patch blocks) per workgroup, DM_VOLUME_NT=0 plain stores.
 template <typename OT>
-static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st)
+static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st,
+                            int have_mm = 0)
 {
     const char *impl = getenv("DM_VOLUME_IMPL");
     if ((impl && impl[0] == 'c') || !volume_ls_eligible(b)) return DM_ERR_UNSUPPORTED;
@@ -1349,11 +1350,11 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
     if (nw4o5 && G == 8 && nt) {
-        k_volume_ls<8, 4, true, OT, 5><<<grid, 256, 0, st>>>(gg, s, Bw, QS, out);
+        k_volume_ls<8, 4, true, OT, 5><<<grid, 256, 0, st>>>(gg, s, Bw, QS, out, have_mm);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
-#define DM_VL(G_, NW_, NT_) if (G == G_ && nw == NW_ && nt == NT_) { k_volume_ls<G_, NW_, NT_, OT><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, out); HIP_TRY(hipGetLastError()); return DM_OK; }
+#define DM_VL(G_, NW_, NT_) if (G == G_ && nw == NW_ && nt == NT_) { k_volume_ls<G_, NW_, NT_, OT><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_VL(2, 8, true) DM_VL(4, 8, true) DM_VL(8, 8, true) DM_VL(16, 8, true)
     DM_VL(8, 4, true) DM_VL(16, 4, true) DM_VL(8, 8, false) DM_VL(16, 8, false)
 #undef DM_VL
@@ -1362,7 +1363,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
 
 extern "C" {
 
-int dm_abi_version(void) { return 104; }
+int dm_abi_version(void) { return 105; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1466,7 +1467,7 @@ int dm_corr_level12(const dm_tiles *b, void *d_stats, double *d_level1, double *
     return launch_mfq<true>(b, d_stats, d_level1, d_level2, (hipStream_t)stream);
 }
 
-int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
+static int volume_f32(const dm_tiles *b, void *d_stats, float *d_l0, void *stream, int have_mm)
 {
     int rc = check_tiles(b);
     if (rc) return rc;
@@ -1478,7 +1479,7 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
-        if (launch_volume_ls<float>(b, d_stats, s, d_l0, (hipStream_t)stream) == DM_OK) return DM_OK;
+        if (launch_volume_ls<float>(b, d_stats, s, d_l0, (hipStream_t)stream, have_mm) == DM_OK) return DM_OK;
         const char *cs = getenv("DM_VOLUME_CS");
         const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
         const bool bf = mfma_bf16(b);
@@ -1539,7 +1540,7 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
     return DM_OK;
 }
 
-int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream)
+static int volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream, int have_mm)
 {
     int rc = check_tiles(b);
     if (rc) return rc;
@@ -1552,7 +1553,7 @@ int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *s
         dm_v4i *Bw;
         int2 *QS;
         mfma_views(b, d_stats, &Bw, &QS);
-        if (launch_volume_ls<_Float16>(b, d_stats, s, out, st) == DM_OK) return DM_OK;
+        if (launch_volume_ls<_Float16>(b, d_stats, s, out, st, have_mm) == DM_OK) return DM_OK;
         const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
         if (b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
             // the float32 column-split kernel with a binary16 stage: 4 rows per store burst
@@ -1584,6 +1585,24 @@ int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *s
     k_volume<_Float16><<<grid, 256, 0, st>>>(make_geo(b), s, out);
     HIP_TRY(hipGetLastError());
     return DM_OK;
+}
+
+int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream)
+{
+    return volume_f32(b, d_stats, d_l0, stream, 0);
+}
+
+int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream)
+{
+    return volume_f16(b, d_stats, d_l0, stream, 0);
+}
+
+int dm_corr_volume_ex(const dm_tiles *b, void *d_stats, int32_t flags, void *d_l0, void *stream)
+{
+    if (flags & ~(DM_VOLUME_F16 | DM_VOLUME_MINMAX_KNOWN)) return fail(DM_ERR_ARG, "unknown volume flags 0x%x", flags);
+    const int mm = (flags & DM_VOLUME_MINMAX_KNOWN) != 0;
+    if (flags & DM_VOLUME_F16) return volume_f16(b, d_stats, (uint16_t *)d_l0, stream, mm);
+    return volume_f32(b, d_stats, (float *)d_l0, stream, mm);
 }
 
 int dm_rectify_f16(const uint16_t *d_in, size_t n, double *d_out, void *stream)

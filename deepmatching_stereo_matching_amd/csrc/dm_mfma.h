@@ -1167,8 +1167,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 // ===================================================================================
 template <int G, int NW, bool NT, typename OT, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                   const int2 *__restrict__ QS, OT *vol)
+                                                   const int2 *__restrict__ QS, OT *vol, int have_mm)
 {
+    // have_mm: the per-patch rmin / rmax are already in the statistics workspace (written by
+    // dm_corr_level1/12 or an earlier volume launch on the same stats): sweep 1 -- the MFMA,
+    // y and min/max over every window, ~40 % of this kernel's issue cycles -- is skipped and
+    // the normalisation constants are read back instead (bit-identical: the same rmin/rmax).
     constexpr int W0 = 16 * G;
     constexpr int BUF = G * 1024;          // one row: G B tiles (window stats inside, qs_of_frag)
     constexpr int NL = G;                  // LDS-DMA instructions per row per workgroup
@@ -1225,6 +1229,28 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, q2, n, y);
     };
 
+    float lo[4], hi[4], rmn[4], den[4], rinv[4];
+    bool clamp = false;   // does any r = y * a_p of this wave leave [-1, 1]?
+    const bool cc = g.method == DM_TM_CCOEFF;
+    if (have_mm) {
+        // sweep 2 reads row 0 from buffer h0 & 1 (where sweep 1 would have left it)
+        fill(0, h0 & 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+            rmn[r] = s.rmn[tb + p];
+            const float rmx = s.rmx[tb + p];
+            den[r] = __fsub_rn(rmx, rmn[r]);
+            rinv[r] = __frcp_rn(den[r]);
+            lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
+            hi[r] = cc ? INFINITY : 1.0f;
+            // conservative: rmin / rmax are already clamped, so a bound at +-1 may hide an r
+            // beyond it -- take the clamped sweep then (it is the exact formula either way)
+            clamp = clamp || (!cc && (ap[r] == 0.0f || rmx >= 1.0f || rmn[r] <= -1.0f));
+        }
+        clamp = __builtin_amdgcn_ballot_w64(clamp) != 0;
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
     fill(0, 0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -1248,8 +1274,6 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         }
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    float lo[4], hi[4], rmn[4], den[4], rinv[4];
-    bool clamp = false;   // does any r = y * a_p of this wave leave [-1, 1]?
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         for (int off = 1; off < 16; off <<= 1) {
@@ -1260,7 +1284,6 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         const float rmx = r_of_y(mx[r], ap[r], g.method);
         den[r] = __fsub_rn(rmx, rmn[r]);
         rinv[r] = __frcp_rn(den[r]);
-        const bool cc = g.method == DM_TM_CCOEFF;
         lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
         hi[r] = cc ? INFINITY : 1.0f;
         // y * a_p is monotone in y (a_p >= 0), so every r of the patch lies in
@@ -1275,6 +1298,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         }
     }
     clamp = __builtin_amdgcn_ballot_w64(clamp) != 0;   // wave-uniform
+    }
 
     // ---- sweep 2: x of every window; lane c holds windows G c .. G c + G - 1 of each of its
     // 4 patches, stored in 16-B pieces (CH tiles) straight from registers ----

@@ -198,28 +198,31 @@ class DevicePyramid:
         h, w = self.b.h0 >> k, self.b.w0 >> k
         return (h, w, h, w)
 
+    def _volume_into(self, v, f16):
+        """dm_corr_volume_ex into v; once the level kernel (or an earlier volume call) has left
+        the per-patch min/max in the stats workspace, the volume kernel reuses them
+        (DM_VOLUME_MINMAX_KNOWN) instead of sweeping every window a second time."""
+        self.compute_stats()
+        flags = (L.DM_VOLUME_F16 if f16 else 0) | (L.DM_VOLUME_MINMAX_KNOWN if self._have_minmax else 0)
+        L.check(self.lib.dm_corr_volume_ex(self.b.ref(), L.ptr(self.stats), flags, L.ptr(v), self._s()),
+                'dm_corr_volume_ex')
+        self._have_minmax = True
+        return v
+
     def volume(self):
         """Level-0 min-max volume (co_map before rectification), float32 [T][P][P]."""
         if self._volume is None:
-            self.compute_stats()
             b = self.b
-            v = torch.empty((b.T, b.P, b.P), dtype=torch.float32, device=b.device)
-            L.check(self.lib.dm_corr_volume(b.ref(), L.ptr(self.stats), L.ptr(v), self._s()),
-                    'dm_corr_volume')
-            self._have_minmax = True
-            self._volume = v
+            self._volume = self._volume_into(torch.empty((b.T, b.P, b.P), dtype=torch.float32,
+                                                         device=b.device), False)
         return self._volume
 
     def volume_f16(self):
         """The level-0 min-max volume as binary16 (dm_corr_volume_f16, BASELINE config C5's
         fp16 correlation): float16 [T][P][P], each value np.float16 of volume()'s."""
-        self.compute_stats()
         b = self.b
-        v = torch.empty((b.T, b.P, b.P), dtype=torch.float16, device=b.device)
-        L.check(self.lib.dm_corr_volume_f16(b.ref(), L.ptr(self.stats), L.ptr(v), self._s()),
-                'dm_corr_volume_f16')
-        self._have_minmax = True
-        return v
+        return self._volume_into(torch.empty((b.T, b.P, b.P), dtype=torch.float16, device=b.device),
+                                 True)
 
     def materialized_levels(self, l0_dtype='f32'):
         """co_map_list built the reference's way (misc/Correlation_map.py:132-156): level 0

@@ -109,6 +109,22 @@ int dm_corr_volume(const dm_tiles *b, void *d_stats, float *d_l0, void *stream);
  * Needs dm_corr_stats first. */
 int dm_corr_volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *stream);
 
+/* Flags of dm_corr_volume_ex. */
+enum {
+    DM_VOLUME_F16 = 1,            /* binary16 output (dm_corr_volume_f16), else float32     */
+    DM_VOLUME_MINMAX_KNOWN = 2    /* d_stats already holds the per-patch min/max: written by
+                                     dm_corr_level1 / dm_corr_level12 / a volume call on the
+                                     same tiles and stats.  The kernel then skips its own
+                                     min/max sweep (the same values: bit-identical output).  */
+};
+
+/* dm_corr_volume / dm_corr_volume_f16 with flags: the same level-0 volume, and, with
+ * DM_VOLUME_MINMAX_KNOWN, without re-deriving the per-patch min/max that an earlier call
+ * left in d_stats -- the reference's co_map read after Correlation_map()() has built the
+ * pyramid (bad_matching.py:62-70 reads it before; Correlation_map.py:69-87 computes both
+ * in one pass).  d_l0: float * or uint16_t * by DM_VOLUME_F16. */
+int dm_corr_volume_ex(const dm_tiles *b, void *d_stats, int32_t flags, void *d_l0, void *stream);
+
 /* d_out[i] = (double)half(d_in[i]) ** 1.4: _rectification (:158-159) of an fp16 volume. */
 int dm_rectify_f16(const uint16_t *d_in, size_t n, double *d_out, void *stream);
 
@@ -222,10 +238,10 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 104 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 105 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
- * carried inside the operand tiles). */
+ * carried inside the operand tiles, 1.5 dm_corr_volume_ex). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

@@ -463,6 +463,50 @@ def test_volume_f16_is_rounded_f32(h0, w0, ws, method):
     feat = 'cv2.TM_CCOEFF_NORMED' if method == 5 else 'cv2.TM_CCOEFF'
     l0 = O.corr_l0(a[:h0 + ws - 1, :w0 + ws - 1], b[:h0 + ws - 1, :w0 + ws - 1], ws, feat)
     _same(v16[0], l0.reshape(h0 * w0, h0 * w0).astype(np.float16))
+    _same(v32[0], l0.reshape(h0 * w0, h0 * w0))     # v32: the min/max-known path (after v16)
+
+
+@pytest.mark.parametrize('h0,w0,ws', [(32, 32, 5), (128, 128, 5), (64, 256, 5), (64, 64, 3), (32, 128, 7)])
+@pytest.mark.parametrize('method', [5, 4])
+@pytest.mark.parametrize('same', [False, True])
+def test_volume_minmax_known_bit_identical(h0, w0, ws, method, same):
+    """dm_corr_volume_ex(DM_VOLUME_MINMAX_KNOWN) -- the per-patch min/max read back from the
+    stats workspace (left there by the level kernel or an earlier volume call) instead of a
+    second sweep over every window -- gives the standalone kernel's volume bit for bit, in
+    float32 and binary16.  same=True pairs an image with itself (r = 1 exactly at q = p:
+    the clamped sweep), plus a constant block (NaN rows, a_p = 0)."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=3 * h0 + w0 + ws + method, dx=2, sinusoidal=True)
+    if same:
+        b = a.copy()
+        a = a.copy()
+        a[1:1 + ws + 1, 3:3 + ws] = 90
+    org = [(0, 0), (4, 8)]
+    batch = engine.TileBatch(a, b, org, h0, w0, ws, method)
+    lib = L.load()
+    fresh = engine.DevicePyramid(batch, build=False).compute_stats()
+    ref32 = torch.empty((2, h0 * w0, h0 * w0), dtype=torch.float32, device='cuda')
+    ref16 = torch.empty((2, h0 * w0, h0 * w0), dtype=torch.float16, device='cuda')
+    L.check(lib.dm_corr_volume_ex(batch.ref(), L.ptr(fresh.stats), 0, L.ptr(ref32), L.stream_handle()))
+    L.check(lib.dm_corr_volume_ex(batch.ref(), L.ptr(fresh.stats), L.DM_VOLUME_F16, L.ptr(ref16),
+                                  L.stream_handle()))
+    r32, r16 = ref32.cpu().numpy(), ref16.cpu().numpy()
+    del ref32, ref16
+    # min/max from the level kernel (a built pyramid), then both volumes reuse them
+    pyr = engine.DevicePyramid(batch)
+    v32 = pyr.volume().cpu().numpy()
+    v16 = pyr.volume_f16().cpu().numpy()
+    _same(v32, r32)
+    _same(v16, r16)
+    # and from an earlier volume launch on the same stats
+    got = torch.empty((2, h0 * w0, h0 * w0), dtype=torch.float32, device='cuda')
+    L.check(lib.dm_corr_volume_ex(batch.ref(), L.ptr(fresh.stats), L.DM_VOLUME_MINMAX_KNOWN, L.ptr(got),
+                                  L.stream_handle()))
+    _same(got.cpu().numpy(), r32)
+    with pytest.raises(Exception):
+        L.check(lib.dm_corr_volume_ex(batch.ref(), L.ptr(fresh.stats), 8, L.ptr(got), L.stream_handle()))
 
 
 @pytest.mark.parametrize('h0,w0,ws', [(32, 32, 5), (64, 64, 5), (16, 64, 3)])

@@ -84,14 +84,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('asm')
     ap.add_argument('kernel')
-    ap.add_argument('--weights')
+    ap.add_argument('--weights', help='JSON {"block": executions per wave}; unlisted blocks count '
+                                      '"_default" (1 if absent)')
     ap.add_argument('--waves', type=float, default=1.0, help='waves per launch (to scale the totals)')
     args = ap.parse_args()
     bl = blocks(kernel_lines(args.asm, args.kernel))
     w = json.load(open(args.weights)) if args.weights else None
     tot_i = tot_c = 0.0
     for k, b in bl:
-        n = (w or {}).get(k, 0 if w else 1)
+        n = (w or {}).get(k, (w or {}).get('_default', 1))
         tot_i += n * (b['valu'] + b['mfma'])
         tot_c += n * b['cycles']
         top = sorted(b['ops'].items(), key=lambda kv: -kv[1])[:6]

@@ -27,6 +27,9 @@ def main():
     ap.add_argument('--tile', type=int, default=128)
     ap.add_argument('--tiles', type=int, default=32)
     ap.add_argument('--f16', action='store_true', help='time dm_corr_volume_f16 (binary16, 2 B/voxel)')
+    ap.add_argument('--mm', action='store_true',
+                    help='min/max already in the stats (one untimed standalone launch first), timed with '
+                         'dm_corr_volume_ex(DM_VOLUME_MINMAX_KNOWN)')
     args = ap.parse_args()
     S, ws = args.tile, 5
     side = 9 * S + ws - 1
@@ -40,6 +43,12 @@ def main():
     pyr = engine.DevicePyramid(batch, build=False).compute_stats()
     vol = torch.empty((batch.T, batch.P, batch.P), dtype=torch.float16 if args.f16 else torch.float32, device=dev)
     fn = lib.dm_corr_volume_f16 if args.f16 else lib.dm_corr_volume
+    if args.mm:
+        L.check(fn(batch.ref(), L.ptr(pyr.stats), L.ptr(vol), L.stream_handle()))
+        flags = (L.DM_VOLUME_F16 if args.f16 else 0) | L.DM_VOLUME_MINMAX_KNOWN
+
+        def fn(b_, st_, v_, s_):   # noqa: F811
+            return lib.dm_corr_volume_ex(b_, st_, flags, v_, s_)
     res = {v: [] for v in args.variants.split(',')}
     for rnd in range(args.rounds + 1):
         for v in res:
