@@ -252,11 +252,22 @@ __device__ __forceinline__ float dpp_prev16_or(float v, float old)
 }
 
 // one 16x16 tile: i8 MFMA onto acc0 (YF bias) or, BF, the bf16 MFMA whose f32 accumulator
-// is exact (integer partial sums < 2^24) -- returned as raw bits either way
-template <int KS, bool BF>
+// is exact (integer partial sums < 2^24) -- returned as raw bits either way.
+// K32 (spread layout: KS == 1, n <= 32): the taps sit in bytes 0..7 of every lane, 8 per
+// lane group -- exactly v_mfma_i32_16x16x32_i8's operand layout (k = 8 (lane >> 4) + j) -- so
+// the K = 32 instruction on the low 8 bytes gives the same exact sums as the K = 64 one (whose
+// bytes 8..15 are A's zeros against the window stats).  On gfx950 an MFMA keeps its SIMD
+// from issuing VALU while it runs (profiles/r03_valu_probe.txt), and the K = 32 form runs
+// half as long.
+template <int KS, bool BF, bool K32 = false>
 __device__ __forceinline__ dm_v4i mfma_tile(const dm_v4i *A, const dm_v4i *Bf, dm_v4i acc0)
 {
-    if constexpr (BF) {
+    if constexpr (K32 && !BF) {
+        static_assert(KS == 1, "K = 32 form: one spread-layout fragment");
+        const long a = (long)(((unsigned long)(unsigned)A[0].y << 32) | (unsigned)A[0].x);
+        const long b = (long)(((unsigned long)(unsigned)Bf[0].y << 32) | (unsigned)Bf[0].x);
+        return __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, acc0, 0, 0, 0);
+    } else if constexpr (BF) {
         typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
         typedef float v4f __attribute__((ext_vector_type(4)));
         v4f c = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -554,7 +565,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto minmax_row = [&](const RowFrag &f) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, BF, EQ>(A, f.b[tw], acc0);
             float y[4];
             y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
@@ -622,7 +633,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&last)[4]) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma_tile<KS, BF>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, BF, EQ>(A, f.b[tw], acc0);
             float y[4];
             y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
@@ -1226,7 +1237,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
         const dm_f2 q2 = qs_of_frag(bf); // {qx, qy}
         dm_v4i bfr[1] = {bf};
-        y_of_acc<true, false>(mfma_tile<1, false>(A, bfr, acc0), sTr, sTf, q2, n, y);
+        y_of_acc<true, false>(mfma_tile<1, false, true>(A, bfr, acc0), sTr, sTf, q2, n, y);
     };
 
     float lo[4], hi[4], rmn[4], den[4], rinv[4];

@@ -11,9 +11,10 @@ instruction on one SIMD, many waves):
        v_mul_i32_i24, DPP forms, converts, frexp / ldexp, VOP3 integer forms (bfe, and_or,
        lshl_add, mad_u32_u24, mul_lo), the cheap ops above with an SGPR operand, all else
   8    transcendental, v_permlane32_swap
-  16   v_mfma_i32_16x16x64_i8: it holds its SIMD's vector issue for its whole 16 cycles
-       (profiles/r03_valu_probe.txt: one MFMA + N independent v_fma_f32 per step takes
-       16 + 2.2 N cycles)
+  14   v_mfma_i32_16x16x64_i8 and 11.2 v_mfma_i32_16x16x32_i8: what one MFMA adds to a stream of
+       independent VALU work on its SIMD (profiles/r03_valu_probe.txt: one MFMA + N v_fma_f32 per
+       step takes ~13.4 + 2.4 N cycles for K=64 and ~11.2 + 2.2 N for K=32, N = 4..12; both take
+       16 cycles alone)
 
 and, given per-block execution counts per wave (--weights file: {"block": count}), the
 modelled issue cycles per wave.  Without weights it prints the per-block table, which is
@@ -34,7 +35,7 @@ TRANS = re.compile(r'^v_(exp|log|rcp|rsq|sqrt|sin|cos)_f32|^v_permlane32_swap')
 
 def cost(op, line):
     if op.startswith('v_mfma'):
-        return 16.0
+        return 11.2 if '16x16x32' in op else 14.0
     if TRANS.match(op):
         return 8.0
     if CHEAP.match(op) and 'dpp' not in line and '_e64' not in op and not SGPR.search(line.split(None, 1)[-1]):

@@ -202,6 +202,12 @@ __global__ __launch_bounds__(256) void p_mfma_mix2(float *out, float a, float b)
                 acc4[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, A), __builtin_bit_cast(v8h, B), acc4[k], 0, 0, 0);
             else if constexpr (K == 2)
                 acci[k] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acci[k], 0, 0, 0);
+            else if constexpr (K == 4) {  // i8 16x16x32 (8-byte operands)
+                typedef int v4i_ __attribute__((ext_vector_type(4)));
+                v4i_ r = __builtin_bit_cast(v4i_, acc4[k]);
+                r = __builtin_amdgcn_mfma_i32_16x16x32_i8(((long)A.y << 32) | (unsigned)A.x, ((long)B.y << 32) | (unsigned)B.x, r, 0, 0, 0);
+                acc4[k] = __builtin_bit_cast(v4f, r);
+            }
             else
                 accf[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, A), __builtin_bit_cast(v8bf, B), accf[k], 0, 0, 0);
 #pragma unroll
@@ -341,7 +347,8 @@ int main()
     run_mix("mfma+6", p_mfma_mix<6>, d, 6);
     run_mix("mfma+8", p_mfma_mix<8>, d, 8);
     run_mix("mfma+12", p_mfma_mix<12>, d, 12);
-    const char *nm[4] = {"bf16_16x32", "f16_16x32", "i8_32x32x32", "bf16_32x16"};
+    const char *nm[5] = {"bf16_16x32", "f16_16x32", "i8_32x32x32", "bf16_32x16", "i8_16x16x32"};
+    run_mix(nm[4], p_mfma_mix2<4, 0>, d, 0); run_mix(nm[4], p_mfma_mix2<4, 4>, d, 4); run_mix(nm[4], p_mfma_mix2<4, 8>, d, 8);
     run_mix(nm[0], p_mfma_mix2<0, 0>, d, 0); run_mix(nm[0], p_mfma_mix2<0, 4>, d, 4); run_mix(nm[0], p_mfma_mix2<0, 8>, d, 8);
     run_mix(nm[1], p_mfma_mix2<1, 0>, d, 0); run_mix(nm[1], p_mfma_mix2<1, 4>, d, 4); run_mix(nm[1], p_mfma_mix2<1, 8>, d, 8);
     run_mix(nm[2], p_mfma_mix2<2, 0>, d, 0); run_mix(nm[2], p_mfma_mix2<2, 8>, d, 8); run_mix(nm[2], p_mfma_mix2<2, 16>, d, 16);
