@@ -68,6 +68,12 @@ def parse():
     ap.add_argument('--warmup', type=int, default=5)   # the clock settles after ~3 launches
     ap.add_argument('--streams', type=int, default=2,
                     help='HIP streams consecutive pair solves are pipelined over (1: no overlap)')
+    ap.add_argument('--level-stream', type=int, default=0,
+                    help='1: the level kernels of all solves run on one stream of their own')
+    ap.add_argument('--stats-stream', type=int, default=0,
+                    help='1 (with --level-stream 1): stats of all solves on one stream of their own')
+    ap.add_argument('--pair-priority', choices=('normal', 'high'), default='normal',
+                    help='priority of the pair streams (stats, levels >= 3, matching, stitch)')
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
                     help='BASELINE.json configs: c2 (512^2, S=64), c3 (1024^2, S=128; the metric), '
                          'c4 (64 pairs of c3 per step, sharded over the ranks), c5 (4096^2, S=256)')
@@ -111,7 +117,7 @@ class PairSolver:
                                       L.DM_TM_CCOEFF_NORMED, self.dev)
         self.ev = []
 
-    def step(self, timed=False, stream=None, wait=None):
+    def step(self, timed=False, stream=None, wait=None, level_stream=None, stats_stream=None):
         """One full solve of the pair on `stream` (default: the current stream).  Every
         device buffer belongs to this step's DevicePyramid, so steps on different streams
         share only the read-only images.  `wait`: event the level kernel waits for (the
@@ -119,9 +125,11 @@ class PairSolver:
         solve's level-kernel end is left in self.last_end."""
         if stream is not None:
             with torch.cuda.stream(stream):
-                return self.step(timed=timed, wait=wait)
+                return self.step(timed=timed, wait=wait, level_stream=level_stream,
+                                 stats_stream=stats_stream)
         from deepmatching_stereo_matching_amd import shard
-        match = self.compute(timed=timed, wait=wait)
+        match = self.compute(timed=timed, wait=wait, level_stream=level_stream,
+                             stats_stream=stats_stream)
         if self.world > 1:   # rank 0 receives every tile's (3, S, S) result and stitches
             match = shard.gather_units_to(match, self.T, self.rank, self.world, 0)
             if match is None:
@@ -129,15 +137,15 @@ class PairSolver:
         return engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                              ['elevation'])
 
-    def compute(self, timed=False, wait=None):
+    def compute(self, timed=False, wait=None, level_stream=None, stats_stream=None):
         """This rank's tiles: stats, dm_corr_level12 [timed], dm_aggregate levels 3.., matching
         with sub-pixel -> float64 [T_rank][3][S][S] on the current stream."""
-        pyr = engine.DevicePyramid(self.batch, build=False)
+        pyr = engine.DevicePyramid(self.batch, build=False, stats_stream=stats_stream)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         if timed:
             self.ev.append(ev)
         self.last_end = ev[1]
-        pyr.build(events=ev, wait=wait, nlev=self.levels)
+        pyr.build(events=ev, wait=wait, nlev=self.levels, level_stream=level_stream)
         return pyr.match(sub_pix=True, nlev=self.levels)
 
     def level1_ms(self):
@@ -275,11 +283,13 @@ def level_roofline(solver, tile, l1_ms):
     launch, on the launch stream); peak = 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md max clock).
     The issue cycles per launch are a model (source 'profile'): the kernel's ISA, each
     instruction priced by what tools/valu_probe.hip measured on gfx950 (2.2 cycles for the
-    simple VOP2/VOP1 32-bit ops, 4 for float64, packed float32, VOP3 and DPP forms, 8 for an
-    MFMA's hold on its SIMD), times how often each block runs (tools/isa_cost.py,
+    simple VOP2/VOP1 32-bit ops, 4 for float64, packed float32, VOP3 and DPP forms, 11.2 for a
+    v_mfma_i32_16x16x32_i8's hold on its SIMD), times how often each block runs (tools/isa_cost.py,
     profiles/pmc_level1.json: the modelled instruction count is checked against the PMC
-    SQ_INSTS_VALU of the same build).  frac_at_profiled_clock uses the clock the chip held in
-    the committed PMC pass (GRBM_GUI_ACTIVE / 8 / kernel time) instead of 2.4 GHz.
+    SQ_INSTS_VALU of the same build).  clock_ghz_at_full_issue = achieved / 1024: the clock at
+    which the live time would mean every SIMD issued on every cycle (MI355X holds 1.7-2.3 GHz
+    under this load); issue_occupancy_profiled = the modelled cycles over the cycles of the
+    committed PMC pass's own launch (its GRBM_GUI_ACTIVE / 8), a measured busy fraction.
     valu_busy_pmc (SQ_ACTIVE_INST_VALU x 4 / (1024 x cycles)) prices every VALU instruction at
     4 cycles: an upper bound, kept for comparison with round 2."""
     mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
@@ -293,9 +303,15 @@ def level_roofline(solver, tile, l1_ms):
     if cyc:
         achieved = cyc / (l1_ms * 1e-3) / 1e9
         roof.update({'achieved': round(achieved, 1), 'frac': round(achieved / peak, 4)})
-        if pmc.get('clock_ghz'):
-            roof['frac_at_profiled_clock'] = round(achieved / (1024 * pmc['clock_ghz']), 4)
-            roof['profiled_clock_ghz'] = pmc['clock_ghz']
+        # the clock at which this live time would keep every SIMD issuing on every cycle
+        roof['clock_ghz_at_full_issue'] = round(achieved / 1024, 4)
+        if pmc.get('gpu_cycles_per_launch'):
+            # the same model over the profiled launch's own cycles (GRBM_GUI_ACTIVE / 8 XCDs):
+            # one run's time and clock, not this run's time with another run's clock
+            roof['issue_occupancy_profiled'] = {
+                'value': round(cyc / (1024 * pmc['gpu_cycles_per_launch']), 4),
+                'clock_ghz': pmc.get('clock_ghz'), 'kernel_ms': pmc.get('kernel_ms_profiled'),
+                'source': 'profile: issue cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of the PMC pass'}
         roof['source'] = {'time': 'live: HIP events around every timed launch on its stream',
                           'issue_cycles_per_launch': 'profile: ' + pmc.get('issue_model_note', ''),
                           'peak': '1024 SIMDs x 2.4 GHz, MI355X_MICROARCH.md'}
@@ -443,7 +459,14 @@ def main():
     # collectives run in issue order on its own communication stream, each waiting for the
     # issuing stream, so solves on two streams gather in order.
     nstreams = max(1, args.streams)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)] if nstreams > 1 else [None]
+    prio = -1 if args.pair_priority == 'high' else 0
+    streams = ([torch.cuda.Stream(device=dev, priority=prio) for _ in range(nstreams)]
+               if nstreams > 1 else [None])
+    # --level-stream: every solve's level kernel goes to one more stream (serialised there,
+    # no cross-pair event), so a pair's stats never wait behind the previous pair's tail
+    lstream = torch.cuda.Stream(device=dev) if (args.level_stream and nstreams > 1) else None
+    # --stats-stream: every solve's stats + window operands on one more stream, ahead of it
+    sstream = torch.cuda.Stream(device=dev) if (args.stats_stream and lstream is not None) else None
     nsolve = [0]
     prev_end = [None]
 
@@ -451,7 +474,8 @@ def main():
         for s in solvers:
             st = streams[nsolve[0] % len(streams)]
             nsolve[0] += 1
-            s.step(timed=timed, stream=st, wait=prev_end[0] if st is not None else None)
+            wait = prev_end[0] if (st is not None and lstream is None) else None
+            s.step(timed=timed, stream=st, wait=wait, level_stream=lstream, stats_stream=sstream)
             prev_end[0] = s.last_end
 
     def run(steps, warmup, timed=True):
@@ -542,7 +566,9 @@ def main():
                           'window_size': WS, 'pyramid_levels': args.levels or 'full',
                           'pairs_per_step': job_pairs,
                           'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
-                          'streams': nstreams},
+                          'streams': nstreams, 'level_stream': bool(lstream is not None),
+                          'stats_stream': bool(sstream is not None),
+                          'pair_priority': args.pair_priority},
                'roofline': roof,
                'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
         if k_level:

@@ -95,7 +95,11 @@ class DevicePyramid:
          until ``level(1)`` asks for it) and matching evaluates it on demand.
     levels[l] for the others are float64 [T][Pl][Pl] tensors."""
 
-    def __init__(self, batch, stream=None, build=True, fuse_level2=None):
+    def __init__(self, batch, stream=None, build=True, fuse_level2=None, stats_stream=None):
+        """stats_stream: optional stream the per-patch stats and window operands
+        (dm_corr_stats) are computed on, ahead of this pyramid's own stream -- a caller
+        pipelining pairs keeps them off the pair streams, where they would queue behind the
+        previous pair's matching."""
         self.b = batch
         self.lib = L.load()
         try:   # a shape the pyramid rejects can still give its level-0 volume (bad_matching.py)
@@ -103,8 +107,17 @@ class DevicePyramid:
         except ValueError as e:
             self._plan = e
         self.stream = stream
-        self.stats = torch.empty(self.lib.dm_stats_bytes(batch.ref()), dtype=torch.uint8,
-                                 device=batch.device)
+        self._stats_stream = stats_stream
+        self._stats_ready = None
+        nbytes = self.lib.dm_stats_bytes(batch.ref())
+        if stats_stream is None:
+            self.stats = torch.empty(nbytes, dtype=torch.uint8, device=batch.device)
+        else:
+            # from the stats stream's pool; every other stream that touches it is recorded, so
+            # the caching allocator reuses it only after their work on it has finished
+            with torch.cuda.stream(stats_stream):
+                self.stats = torch.empty(nbytes, dtype=torch.uint8, device=batch.device)
+            self.stats.record_stream(stream if stream is not None else torch.cuda.current_stream())
         if fuse_level2 is None:
             fuse_level2 = int(os.environ.get('DM_FUSE_L2', str(FUSE_DEFAULT)))
         self.fuse_level2 = int(fuse_level2)
@@ -134,8 +147,15 @@ class DevicePyramid:
 
     def compute_stats(self):
         if not self._have_stats:
-            L.check(self.lib.dm_corr_stats(self.b.ref(), L.ptr(self.stats), self._s()),
+            ss = self._stats_stream
+            L.check(self.lib.dm_corr_stats(self.b.ref(), L.ptr(self.stats),
+                                           L.stream_handle(ss) if ss is not None else self._s()),
                     'dm_corr_stats')
+            if ss is not None:
+                self._stats_ready = torch.cuda.Event()
+                self._stats_ready.record(ss)
+                (self.stream if self.stream is not None else torch.cuda.current_stream()).wait_event(
+                    self._stats_ready)
             self._have_stats = True
         return self
 
@@ -144,14 +164,16 @@ class DevicePyramid:
         Pk = (b.h0 >> k) * (b.w0 >> k)
         return torch.empty((b.T, Pk, Pk), dtype=torch.float64, device=b.device)
 
-    def _level1(self):
-        l1 = self._empty_level(1)
-        L.check(self.lib.dm_corr_level1(self.b.ref(), L.ptr(self.stats), L.ptr(l1), self._s()),
+    def _level1(self, stream=None, l1=None):
+        if l1 is None:
+            l1 = self._empty_level(1)
+        sh = L.stream_handle(stream) if stream is not None else self._s()
+        L.check(self.lib.dm_corr_level1(self.b.ref(), L.ptr(self.stats), L.ptr(l1), sh),
                 'dm_corr_level1')
         self._have_minmax = True
         return l1
 
-    def build(self, events=None, wait=None, nlev=None):
+    def build(self, events=None, wait=None, nlev=None, level_stream=None):
         """Levels >= 1 up to level ``nlev`` - 1 (default: the full pyramid, as
         Correlation_map always builds it; a smaller ``nlev`` is the k-level pyramid of
         BASELINE configs C2/C3, whose levels above k - 1 Matching never reads).  ``events``:
@@ -160,21 +182,44 @@ class DevicePyramid:
         kernel waits for (the stats run before it) -- a caller pipelining pairs over streams
         passes the previous pair's level-kernel end, so the level kernels run one after
         another while each pair's latency-bound tail (levels >= 3, matching, stitch) overlaps
-        the next pair's level kernel.  Building more levels later extends the pyramid."""
+        the next pair's level kernel.  ``level_stream``: optional stream the level kernel runs
+        on (it waits for this pyramid's stats, and this pyramid's stream waits for it): a
+        caller that sends every pair's level kernel to one such stream serialises them without
+        events, and a pair's stats no longer queue behind the previous pair's tail on a shared
+        pair stream.  Building more levels later extends the pyramid."""
         b, lib = self.b, self.lib
         self.compute_stats()
         top = self.nlev if nlev is None else max(1, min(int(nlev), self.nlev))
         if top > 1 and len(self.levels) == 1:
             fused = False
             st = self.stream if self.stream is not None else torch.cuda.current_stream()
+            ls = st
+            if level_stream is not None and level_stream != st:
+                ls = level_stream
+                if self._stats_ready is not None:   # stats on their own stream: wait for them only
+                    ls.wait_event(self._stats_ready)
+                else:
+                    ready = torch.cuda.Event()
+                    ready.record(st)
+                    ls.wait_event(ready)
+                self.stats.record_stream(ls)
             if wait is not None:
-                st.wait_event(wait)
+                ls.wait_event(wait)
             if events:
-                events[0].record(st)
-            if self.fuse_level2 and top >= 3:
-                l2 = self._empty_level(2)
-                l1 = self._empty_level(1) if self.fuse_level2 == 1 else None
-                rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), L.ptr(l1), L.ptr(l2), self._s())
+                events[0].record(ls)
+            # level buffers come from the level stream's pool (st's too when they are one):
+            # st's later use of them is recorded, so the caching allocator reuses them only
+            # after both streams' work on them
+            with torch.cuda.stream(ls):
+                l2 = self._empty_level(2) if (self.fuse_level2 and top >= 3) else None
+                l1 = self._empty_level(1) if (self.fuse_level2 == 1 or l2 is None) else None
+            if ls is not st:
+                for t in (l1, l2):
+                    if t is not None:
+                        t.record_stream(st)
+            if l2 is not None:
+                rc = lib.dm_corr_level12(b.ref(), L.ptr(self.stats), L.ptr(l1), L.ptr(l2),
+                                         L.stream_handle(ls))
                 if rc == L.DM_OK:
                     self.levels += [l1, l2]
                     self._have_minmax = True
@@ -182,9 +227,18 @@ class DevicePyramid:
                 elif rc != L.DM_ERR_UNSUPPORTED:
                     L.check(rc, 'dm_corr_level12')
             if not fused:
-                self.levels.append(self._level1())
+                if l1 is None:
+                    with torch.cuda.stream(ls):
+                        l1 = self._empty_level(1)
+                    if ls is not st:
+                        l1.record_stream(st)
+                self.levels.append(self._level1(ls, l1))
             if events:
-                events[1].record(st)
+                events[1].record(ls)
+            if ls is not st:
+                done = torch.cuda.Event()
+                done.record(ls)
+                st.wait_event(done)
         while len(self.levels) < top:
             k = len(self.levels)               # build level k from level k - 1
             h, w = b.h0 >> (k - 1), b.w0 >> (k - 1)
