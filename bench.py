@@ -460,11 +460,14 @@ def main():
     # issuing stream, so solves on two streams gather in order.
     nstreams = max(1, args.streams)
     prio = -1 if args.pair_priority == 'high' else 0
-    streams = ([torch.cuda.Stream(device=dev, priority=prio) for _ in range(nstreams)]
-               if nstreams > 1 else [None])
     # --level-stream: every solve's level kernel goes to one more stream (serialised there,
-    # no cross-pair event), so a pair's stats never wait behind the previous pair's tail
-    lstream = torch.cuda.Stream(device=dev) if (args.level_stream and nstreams > 1) else None
+    # no cross-pair event), so a pair's stats never wait behind the previous pair's tail.
+    # HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order: a stream sharing a
+    # queue with another waits behind that stream's work, so the pipeline keeps to 3 streams
+    # (1 pair stream + level + stats) or 4.
+    lstream = torch.cuda.Stream(device=dev) if args.level_stream else None
+    streams = ([torch.cuda.Stream(device=dev, priority=prio) for _ in range(nstreams)]
+               if (nstreams > 1 or lstream is not None) else [None])
     # --stats-stream: every solve's stats + window operands on one more stream, ahead of it
     sstream = torch.cuda.Stream(device=dev) if (args.stats_stream and lstream is not None) else None
     nsolve = [0]

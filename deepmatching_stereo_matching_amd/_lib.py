@@ -20,6 +20,7 @@ HEADER = os.path.join(os.path.dirname(HERE), 'include', 'dmstereo.h')
 
 DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3, -4
 DM_VOLUME_F16, DM_VOLUME_MINMAX_KNOWN = 1, 2   # dm_corr_volume_ex flags
+DM_POW_F32, DM_POW_Q4, DM_POW_K, DM_POW_FULL = 0, 1, 2, 3   # dm_pow14_variant forms
 DM_TM_CCOEFF, DM_TM_CCOEFF_NORMED = 4, 5
 METHODS = {'cv2.TM_CCOEFF_NORMED': DM_TM_CCOEFF_NORMED, 'cv2.TM_CCOEFF': DM_TM_CCOEFF}
 CAL_MODES = {'elevation': 0, 'elevation2': 1, 'distance': 2}
@@ -58,6 +59,7 @@ SIGNATURES = {
     'dm_rectify_f16': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_rectify64': ([_P, ctypes.c_size_t, _P, _P], ctypes.c_int),
+    'dm_pow14_variant': ([_I, _P, ctypes.c_size_t, _P, _P], ctypes.c_int),
     'dm_aggregate': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_match': ([_TP, _P, ctypes.POINTER(ctypes.c_void_p), _I, _I, _I, _I, _I, _I, _I, _I,
                   _P, _P, _P], ctypes.c_int),

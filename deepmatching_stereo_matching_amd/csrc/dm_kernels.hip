@@ -486,6 +486,26 @@ __global__ void k_rectify(const F *in, size_t n, double *out)
         out[i] = pow14((double)in[i]);
 }
 
+// the in-kernel pow14 forms on arbitrary inputs (dm_pow14_variant): tables in LDS exactly as
+// the level kernel holds them
+template <int V>
+__global__ __launch_bounds__(256) void k_pow_variant(const double *in, size_t n, double *out)
+{
+    __shared__ PowLds plds;
+    pow_lds_fill(plds, threadIdx.x, 256);
+    __syncthreads();
+    const unsigned mant = mant_mask_vgpr();
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const double x = in[i];
+        double r;
+        if constexpr (V == DM_POW_F32) r = pow14_zf((float)x, plds, mant);
+        else if constexpr (V == DM_POW_Q4) r = pow14_q4(x, plds);
+        else if constexpr (V == DM_POW_K) r = pow14_k(x, plds);
+        else r = pow14_lds(x, plds);
+        out[i] = r;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // pyramid step for levels >= 1 (float64 in, float64 out)
 // ------------------------------------------------------------------------------------
@@ -1132,12 +1152,23 @@ static bool mfma_bf16(const dm_tiles *b)
     return level1_variant(b) == 3 && b->ws <= 5 && e && e[0] == '1';
 }
 
-// waves per workgroup of k_level1_mfq: NW = min(4, G/2); column group width GW = G/NW
+// waves per workgroup of k_level1_mfq (and the window layout dm_corr_stats writes for it):
+// column group width GW = G/NW tiles of 16 windows per wave.  GW = 4 (two pooled columns per
+// lane: the left neighbour of the second is in the lane, level 2 pools in the lane) where the
+// width gives 2 or 4 such waves and the packed-y path applies; GW = 2 otherwise.  Same box,
+// bit-identical (tools/kbench.py, profiles/r03k_*): C3 (S=128) 7.96 -> 7.72 ms with 2 waves of
+// GW = 4 instead of 4 waves of GW = 2 (137 VGPRs: 3 waves/SIMD instead of 5), C5 (S=256)
+// 549 -> 487 ms with 4 waves instead of 8.
 static int mfq_nw(const dm_tiles *b)
 {
+    const int G = b->w0 / 16;
     const char *e = getenv("DM_MFQ_NWMAX"); // A/B knob: 2, 4 or 8 waves per workgroup at most
+    const char *gw = getenv("DM_MFQ_GW");   // A/B knob: 2 forces the GW = 2 layout
     const int cap = (e && e[0] == '4') ? 4 : (e && e[0] == '2') ? 2 : 8;
-    return b->w0 / 16 / 2 < cap ? b->w0 / 16 / 2 : cap;
+    const bool g4 = !(gw && gw[0] == '2') && b->ws * b->ws <= 25 && G % 4 == 0 &&
+                    (G / 4 == 2 || G / 4 == 4) && G / 4 <= cap;
+    if (g4) return G / 4;
+    return G / 2 < cap ? G / 2 : cap;
 }
 
 // second window region: the column-group layout of k_volume_ls (GW = 16 B of output per
@@ -1363,7 +1394,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
 
 extern "C" {
 
-int dm_abi_version(void) { return 105; }
+int dm_abi_version(void) { return 106; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1620,6 +1651,23 @@ int dm_rectify(const float *d_in, size_t n, double *d_out, void *stream)
     if (!d_in || !d_out) return fail(DM_ERR_ARG, "null pointer");
     if (n == 0) return DM_OK;
     k_rectify<float><<<nblk(n, 256) > 8192 ? 8192 : nblk(n, 256), 256, 0, (hipStream_t)stream>>>(d_in, n, d_out);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_pow14_variant(int32_t variant, const double *d_in, size_t n, double *d_out, void *stream)
+{
+    if ((!d_in || !d_out) && n) return fail(DM_ERR_ARG, "null input / output");
+    if (!n) return DM_OK;
+    const unsigned grid = nblk(n, 256) > 1024 ? 1024 : nblk(n, 256);
+    hipStream_t st = (hipStream_t)stream;
+    switch (variant) {
+    case DM_POW_F32: k_pow_variant<DM_POW_F32><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    case DM_POW_Q4: k_pow_variant<DM_POW_Q4><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    case DM_POW_K: k_pow_variant<DM_POW_K><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    case DM_POW_FULL: k_pow_variant<DM_POW_FULL><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    default: return fail(DM_ERR_ARG, "unknown pow14 variant %d", variant);
+    }
     HIP_TRY(hipGetLastError());
     return DM_OK;
 }

@@ -135,6 +135,19 @@ int dm_rectify(const float *d_in, size_t n, double *d_out, void *stream);
 /* Same for float64 input (Correlation_map._rectification on an aggregated map). */
 int dm_rectify64(const double *d_in, size_t n, double *d_out, void *stream);
 
+/* Self-test of the pow14 forms the fused kernels evaluate in place of _rectification
+ * (:158-159), tables in LDS as the kernels hold them.  d_out[i] = form(d_in[i]); each form
+ * equals dm_pow14 (dm_pow.h) bit for bit on its domain, and only there:
+ *   DM_POW_F32   pow14_zf((float)x): 0, NaN and float32-normal x in (0, 1] (the level
+ *                kernel's child values: x is a float32 in [0, 1] or NaN)
+ *   DM_POW_Q4    pow14_q4(s) = pow14(s / 4): s == 0, NaN, or s / 4 in [2^-319, 1] (a sum of
+ *                four children, level-1 / level-2 averaging); 0 < s / 4 < 2^-319 gives 0 and
+ *                s = +inf NaN instead of dm_pow14's values
+ *   DM_POW_K     pow14_k(x): 0, NaN and x in [2^-319, 1]
+ *   DM_POW_FULL  pow14_lds(x): every double (the slow path outside [2^-319, 1]) */
+enum dm_pow_variant { DM_POW_F32 = 0, DM_POW_Q4 = 1, DM_POW_K = 2, DM_POW_FULL = 3 };
+int dm_pow14_variant(int32_t variant, const double *d_in, size_t n, double *d_out, void *stream);
+
 /* One pyramid step for levels >= 1: MaxPool2d(3,2,1) per map, (ul+ur+ll+lr)/4, and
  * (rectify != 0) the 1.4 power.  d_in float64 [T][h*w][h*w] -> d_out float64
  * [T][(h/2)*(w/2)][(h/2)*(w/2)].
@@ -238,10 +251,11 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 105 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 106 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
- * carried inside the operand tiles, 1.5 dm_corr_volume_ex). */
+ * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
+ * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

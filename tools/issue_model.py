@@ -5,8 +5,8 @@ The kernel's ISA (hipcc -S of dm_kernels.hip, the same flags as the library) is 
 basic blocks and priced by tools/isa_cost.py (per-instruction issue cycles measured on
 gfx950 by tools/valu_probe.hip, profiles/r03_valu_probe.txt); each block is weighted by how
 often one wave runs it (profiles/issue_model_level1_{c3,c5}_weights.json, read off the loop
-structure: sweep 1 h0/2 iterations, sweep 2 h0/2 - 2 plus two peeled, the level-2 stash
-every 2nd / 4th / 16th level-1 row).  The weighted instruction count is checked against the
+structure: sweep 1 h0/2 iterations, sweep 2 h0/2 - 2 plus two peeled, level 2 on every
+second level-1 row, the level-2 stash rectified every 4th level-2 row).  The weighted instruction count is checked against the
 PMC SQ_INSTS_VALU of the same build (both count MFMAs); the modelled cycles x waves per
 launch is 'issue_cycles_per_launch'.
 
@@ -23,10 +23,10 @@ sys.path.insert(0, os.path.join(REPO, 'tools'))
 import isa_cost  # noqa: E402
 
 KERNELS = {  # shape -> (kernel symbol substring, weights file, pmc file, waves per launch)
-    'c3': ('k_level1_mfqILi1ELi2ELi4ELi5ELb1ELb1ELb0E', 'issue_model_level1_c3_weights.json',
-           'pmc_level1.json', 64 * (128 // 4) * (128 // 4) * 4),
-    'c5': ('k_level1_mfqILi1ELi2ELi8ELi5ELb1ELb1ELb0E', 'issue_model_level1_c5_weights.json',
-           'pmc_level1_s256.json', 256 * (256 // 4) * (256 // 4) * 8),
+    'c3': ('k_level1_mfqILi1ELi4ELi2ELi5ELb1ELb1ELb0E', 'issue_model_level1_c3_weights.json',
+           'pmc_level1.json', 64 * (128 // 4) * (128 // 4) * 2),
+    'c5': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELb0E', 'issue_model_level1_c5_weights.json',
+           'pmc_level1_s256.json', 256 * (256 // 4) * (256 // 4) * 4),
 }
 
 
