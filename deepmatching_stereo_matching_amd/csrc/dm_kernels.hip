@@ -827,8 +827,8 @@ struct PatchL0 {
 // y (monotone: same as pooling the rectified values), normalises and rectifies the 9 pooled
 // values; the 4 lanes sum them in ul, ur, ll, lr order, /4, rectify -- the arithmetic of
 // k_level1_mfq / k_aggregate, so the window equals the stored level 1 bit for bit.
-template <int WS>
-__global__ __launch_bounds__(256) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
+template <int WS, int MW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
 {
     constexpr int ws = WS, n = WS * WS;
     const int h0 = g.h0, w0 = g.w0;
@@ -1202,9 +1202,18 @@ static inline unsigned nblk(size_t n, unsigned bs)
     return (unsigned)(b > 0x7fffffff ? 0x7fffffff : b);
 }
 
+// DM_TAIL_MINW=6 (A/B knob): the ws = 5 on-demand matching kernels with a 6 waves/SIMD register
+// budget (<= 80 VGPRs), small enough to run beside a level kernel (3 waves of 144 VGPRs per
+// SIMD) instead of waiting for its workgroups to retire
+static bool tail_lean()
+{
+    const char *e = getenv("DM_TAIL_MINW");
+    return e && e[0] == '6';
+}
+
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
-template <int WS>
-__global__ __launch_bounds__(256) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
+template <int WS, int MW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
 {
     const int hn = g.h0, wn = g.w0, h = hn / 2, w = wn / 2;
     const size_t Pp = (size_t)h * w, Pn = (size_t)hn * wn;
@@ -1246,8 +1255,8 @@ __global__ __launch_bounds__(256) void k_match_step_l0(Geo g, Stats s, int T, co
 }
 
 // _sub_pix_cal with level 0 on demand, patch taps in registers (see k_subpix)
-template <int WS>
-__global__ __launch_bounds__(256) void k_subpix_t(Geo g, Stats s, int T, double *map)
+template <int WS, int MW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_subpix_t(Geo g, Stats s, int T, double *map)
 {
     const int h0 = g.h0, w0 = g.w0;
     const size_t P = (size_t)h0 * w0;
@@ -1764,7 +1773,9 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l1<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l1<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: k_match_step_l1<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 5: if (tail_lean()) k_match_step_l1<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                    else k_match_step_l1<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                    break;
             case 7: k_match_step_l1<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l1<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l1<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1778,7 +1789,9 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l0<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l0<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: k_match_step_l0<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
+            case 5: if (tail_lean()) k_match_step_l0<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                    else k_match_step_l0<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                    break;
             case 7: k_match_step_l0<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l0<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l0<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1800,7 +1813,9 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_subpix_t<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 3: k_subpix_t<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
-            case 5: k_subpix_t<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
+            case 5: if (tail_lean()) k_subpix_t<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur]);
+                    else k_subpix_t<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur]);
+                    break;
             case 7: k_subpix_t<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 9: k_subpix_t<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 11: k_subpix_t<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
