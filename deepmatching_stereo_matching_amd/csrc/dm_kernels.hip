@@ -36,12 +36,15 @@ __device__ __forceinline__ double pow14(double x)
 
 // Fast-path tables staged in LDS by the level-1 kernels (gathers with random rows: strides
 // of 8 and 16 B spread over the banks; one 32-B row per index conflicted 4x more, measured):
-//   fc[i], fp[i] = c_i, (1/c_i)^y hi, lo                   per mantissa index
-//   fc32[i]       = c_i as float32 (exact: 10 significant bits), for float32 inputs
+//   fp[i]   = (1/c_i)^y hi, lo                              per mantissa index
+//   fc32[i] = c_i as float32 (exact: 10 significant bits); float64 callers widen it (exact)
 //   gz[k]   = 2^(yE) as {G, g} for E = k - 1 + EMIN (1 <= k < DM_GZ_ROWS);  gz[0] = 0 (x == 0
 //             -> +0);  gz[DM_GZ_ROWS] = NaN (pow14_q4's row for a NaN input)
 //   g32[b]  = 2^(yE) for the f32 biased exponent b = E + 127 (1 <= b <= 127); g32[255] = NaN
-//             (x = NaN -> NaN); else 0
+//             (x = NaN -> NaN); g32[0] = 0.  Rows 128..254 (x > 1) are never read by the
+//             level kernels, whose float32 inputs are in [0, 1] or NaN: with fill(hole = true)
+//             they are left unwritten and the level kernel keeps its own exchange arrays there
+//             (G32_HOLE bytes from &g32[128]), which keeps its LDS within 20 KB.
 // Same constants and the same operation sequence as dm_pow14_fast, so every variant below
 // returns dm_pow14's value on its domain.
 #define DM_GZ_ROWS (2 - DM_POWF_EMIN)
@@ -55,14 +58,13 @@ struct PowLds {
     dm_d2 fp[DM_POWF_NT];
     dm_d2 gz[DM_GZ_ROWS + 1];
     dm_d2 g32[256];
-    double fc[DM_POWF_NT];
     float fc32[DM_POWF_NT]; // c_i has 10 significant bits (gen_pow_tables.py): exact in float32
 };
+constexpr int G32_HOLE = 127 * 16;  // g32 rows 128..254
 
-__device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
+__device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads, bool hole = false)
 {
     for (int i = tid; i < DM_POWF_NT; i += nthreads) {
-        t.fc[i] = c_powf_c[i];
         t.fc32[i] = (float)c_powf_c[i];
         t.fp[i] = dm_d2{c_powf_p[2 * i], c_powf_p[2 * i + 1]};
     }
@@ -71,6 +73,7 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads)
                   : k ? dm_d2{c_powf_g[2 * (k - 1)], c_powf_g[2 * (k - 1) + 1]} : dm_d2{0.0, 0.0};
     }
     for (int b = tid; b < 256; b += nthreads) {
+        if (hole && b >= 128 && b < 255) continue;
         const int e = b - 127 - DM_POWF_EMIN; // row of c_powf_g
         const bool in = b >= 1 && b <= 127 && e >= 0;
         t.g32[b] = in ? dm_d2{c_powf_g[2 * e], c_powf_g[2 * e + 1]}
@@ -94,7 +97,7 @@ __device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const P
 
 __device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
 {
-    return pow14_core_r(fma(M, t.fc[i], -1.0), i, G, t);
+    return pow14_core_r(fma(M, (double)t.fc32[i], -1.0), i, G, t);
 }
 
 // float64 input.  Exact dm_pow14 on [2^EMIN, 1] and 0; other inputs read in-bounds rows and
@@ -1338,7 +1341,10 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
 #define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
     // GW = 4 with 4 waves: 4 waves/SIMD register budget (5 spills)
     if (KS == 1 && GW == 4 && NW == 4) { k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
-    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 2, 8) DM_MQ(1, 4, 2)
+    // GW = 4 with 2 waves (C3): 20 KB of LDS (the exchange arrays in the pow tables' hole)
+    // allow 8 workgroups per CU, so a 4 waves/SIMD register budget (<= 128 VGPRs)
+    if (KS == 1 && GW == 4 && NW == 2) { k_level1_mfq<1, 4, 2, 4, L2F, YF, BF><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 2, 8)
     if constexpr (!YF) {
         DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4) DM_MQ(2, 2, 8)
         DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4) DM_MQ(3, 2, 8)

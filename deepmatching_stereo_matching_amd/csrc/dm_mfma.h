@@ -477,6 +477,17 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds
                  : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
 }
 
+// storage of k_level1_mfq's exchange arrays: its own LDS, or (H) the pow tables' g32 hole
+template <bool H, typename T>
+struct XchOwn {
+    __attribute__((aligned(16))) T v;
+    __device__ T &get(PowLds &) { return v; }
+};
+template <typename T>
+struct XchOwn<true, T> {
+    __device__ T &get(PowLds &p) { return *reinterpret_cast<T *>(&p.g32[128]); }
+};
+
 // L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
 template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
@@ -484,23 +495,34 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 {
     constexpr bool EQ = KS == 1 && YF && !BF;    // window stats ride in the B tile (qs_of_frag)
     __shared__ PowLds plds;
-    // [pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at q1 = 16*GW*(w+1)-1,
-    // slot 0 = -inf (no window left of column 0)
-    __shared__ __attribute__((aligned(16))) float xch[2][2][NW + 1][4][4];
+    // exchange arrays; they live in the pow tables' unused g32 rows when they fit (PowLds),
+    // which keeps the C3 instance (2 waves per workgroup) at <= 20 KB of LDS: 8 workgroups,
+    // 4 waves per SIMD
+    struct Xch {
+        // [pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at
+        // q1 = 16*GW*(w+1)-1, slot 0 = -inf (no window left of column 0)
+        float xch[2][2][NW + 1][4][4];
+        double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: level-2 pow inputs
+        double xch2[2][NW][4];           // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
+    };
+    constexpr bool HOLE = sizeof(Xch) <= G32_HOLE;
+    __shared__ XchOwn<HOLE, Xch> xown;
+    Xch &X = xown.get(plds);
+    auto &xch = X.xch;
+    auto &stash = X.stash;
+    auto &xch2 = X.xch2;
     __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
-    __shared__ double xch2[2][NW][4];  // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
     __shared__ float4 cst[4][6];       // [cell][field][child]: a_p, lo, hi, rmin, den, rinv
     // LATE: the next even row's fragments are loaded after the level-1 emission instead of
     // before it (12 fewer live VGPRs through the emission, less latency cover)
     constexpr bool LATE = L2F;
     constexpr int L2V = 4 * GW, L2B = 64 / L2V; // level-2 values per wave per row; rows per stash
-    __shared__ double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: pow inputs
     // M == 1 (one pooled column per lane, valid on even lanes): the pooled children of RB
     // level-2 rows, [wave][row * 4 * L2V + child * L2V + column], rectified 64 at a time
     constexpr int RB = 64 / (4 * L2V);
-    __shared__ double stash2[L2F && GW == 2 ? NW : 1][64];
+    __shared__ double stash2[L2F && GW == 2 ? NW : 1][L2F && GW == 2 ? 64 : 1];
     const int tid = threadIdx.x;
-    pow_lds_fill(plds, tid, 64 * NW);
+    pow_lds_fill(plds, tid, 64 * NW, HOLE);
     if (tid < 64) (&xch[0][0][0][0][0])[(tid >> 4) * (NW + 1) * 16 + (tid & 15)] = -INFINITY;
     __syncthreads();
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# level kernel in 20 KB of LDS at 4 waves/SIMD (lib_hole) vs the r03m build: parity, then A/B
+R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_pow_gpu.py tests/test_c3_golden.py tests/test_c3_batch.py tests/test_c5_tile.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r03n_gputest.log 2>&1 || exit 1
+for pass in 1 2; do
+  for lib in abl/lib_r03m.so abl/lib_hole.so; do
+    echo "== pass $pass $lib C3"
+    DM_LIB_PATH=$R/$lib timeout -k 10 120 python3 tools/kbench.py --variants l12 --rounds 3 2>&1 | grep -v amdgpu.ids || exit 1
+  done
+done > gpurun_out/r03n_ab.txt
+for lib in abl/lib_r03m.so abl/lib_hole.so; do
+  echo "== $lib C5"
+  DM_LIB_PATH=$R/$lib timeout -k 10 200 python3 tools/kbench.py --variants l12 --rounds 2 --tile 256 --grid 16 2>&1 | grep -v amdgpu.ids || exit 1
+done >> gpurun_out/r03n_ab.txt
