@@ -74,6 +74,7 @@ SIGNATURES = {
                               ctypes.c_int),
     'dm_stitch': ([_P, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_int32), _I, _P, _P, _P],
                   ctypes.c_int),
+    'dm_seq_sum': ([_P, ctypes.c_int64, _P, _P], ctypes.c_int),
 }
 
 _lib = None

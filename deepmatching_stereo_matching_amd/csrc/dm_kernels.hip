@@ -1409,7 +1409,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
 
 extern "C" {
 
-int dm_abi_version(void) { return 106; }
+int dm_abi_version(void) { return 107; }
 
 const char *dm_last_error(void) { return g_err; }
 

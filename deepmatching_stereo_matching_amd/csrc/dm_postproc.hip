@@ -13,7 +13,8 @@
 // sequential order gives it.  One workgroup walks the levels with a barrier between them;
 // the arithmetic per update is the reference's, operation for operation (float64,
 // -ffp-contract=off), so the maps are bit-identical to the sequential loops.  The error
-// sums (`error += abs(...)`) are taken in sequence order by one dependent chain (k_seq_sum).
+// sums (`error += abs(...)`) are the sequence-order float64 sums, bit for bit, computed as
+// integer prefix sums between binade crossings (k_seq_sum_seg).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -282,9 +283,164 @@ __global__ __launch_bounds__(64) void k_seq_sum(const double *__restrict__ v, lo
 
 // (SGPR-fed from wave-uniform s_load blocks instead of readlane measured slower on MI355X:
 // 22 vs 13.8 ms per 1M values -- the chain waits on the scalar loads)
+
+// The same sum without the dependent chain: binade segments.  Every term is >= 0 (an
+// absolute difference), so the running sum s only grows.  While s stays in one binade
+// [2^e, 2^(e+1)) -- ulp u = 2^(e-52); below 2^-1022, u = 2^-1074 -- every partial sum is a
+// multiple of u and a step rounds as RN(s + d) = s + u * inc with inc an integer:
+//   inc = RN(d / u)                       when d / u is not a tie,
+//   inc = floor(d / u) + (p ^ (q & 1))    for a tie (fraction exactly 1/2; q = floor(d / u)),
+// where p = (s / u) mod 2: round-half-even picks the even multiple, and s / u is even after
+// every tie.  (Ties are common: differences of nearby doubles carry few significant bits.)
+// So a run of steps is an integer prefix sum whose increments depend on one parity bit, and
+// that is a scan over the monoid of segments {f: parity in -> parity out, T: parity in ->
+// increment sum}: (A then B).f(p) = B.f(A.f(p)), (A then B).T(p) = A.T(p) + B.T(A.f(p)).
+// One workgroup scans a chunk of 8192 terms in parallel, exactly.  A step is taken by itself,
+// as the reference's one float64 add, where the binade changes: s + inc u reaches 2^(e+1), or
+// d is not finite or not below 2^(e+1) -- once per binade the sum climbs (a few dozen over a
+// sweep).  NaN / inf in s: the rest is added one by one (NaN + x, inf + x as the chain does).
+// Bit-identical to k_seq_sum (tests/test_seq_sum_gpu.py).
+constexpr int SEG_T = 1024, SEG_E = 8, SEG_CH = SEG_T * SEG_E;
+
+struct SegSum {   // a run of steps: parity out and increment sum, for parity in 0 / 1
+    unsigned f0, f1;
+    unsigned long long T0, T1;
+};
+
+__device__ __forceinline__ SegSum seg_then(const SegSum &A, const SegSum &B)
+{
+    SegSum r;
+    r.f0 = A.f0 ? B.f1 : B.f0;
+    r.f1 = A.f1 ? B.f1 : B.f0;
+    r.T0 = A.T0 + (A.f0 ? B.T1 : B.T0);
+    r.T1 = A.T1 + (A.f1 ? B.T1 : B.T0);
+    return r;
+}
+
+__device__ __forceinline__ SegSum seg_shfl_up(const SegSum &x, int o)
+{
+    SegSum r;
+    r.f0 = __shfl_up(x.f0, o);
+    r.f1 = __shfl_up(x.f1, o);
+    r.T0 = __shfl_up(x.T0, o);
+    r.T1 = __shfl_up(x.T1, o);
+    return r;
+}
+
+__global__ __launch_bounds__(SEG_T) void k_seq_sum_seg(const double *__restrict__ v, long long n, double *out)
+{
+    typedef unsigned long long u64;
+    constexpr int NWV = SEG_T / 64;
+    __shared__ SegSum wagg[2][NWV];             // per-wave aggregates (double-buffered)
+    __shared__ long long wmin[2][NWV];          // per-wave first binade change
+    __shared__ double snext[2];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const SegSum ident = {0u, 1u, 0ull, 0ull};
+    double s = 0.0;
+    long long k0 = 0;
+    for (int it = 0; k0 < n; it ^= 1) {
+        if (!(s < INFINITY)) { // NaN or inf (uniform)
+            if (t == 0) {
+                for (long long k = k0; k < n; ++k) s += v[k];
+                *out = s;
+            }
+            return;
+        }
+        // binade of s: u = 2^-sh; its top B = 2^(e+1) = top * u
+        int sh;
+        u64 top;
+        if (s < 0x1p-1022) { sh = 1074; top = 1ull << 52; }
+        else { sh = 52 - ilogb(s); top = 1ull << 53; }
+        const u64 base = (u64)ldexp(s, sh);
+        const double B = ldexp((double)top, -sh);
+        const long long kt = k0 + (long long)t * SEG_E;
+        u64 q[SEG_E];
+        unsigned tie = 0;      // bit i: term i is a tie
+        int lbad = SEG_E;      // the thread's first term that changes the binade by itself
+        SegSum th = ident;
+#pragma unroll
+        for (int i = 0; i < SEG_E; ++i) {
+            const double d = kt + i < n ? v[kt + i] : 0.0;
+            const double f = ldexp(d, sh);    // exact (d < B: f < 2^53)
+            const double fl = floor(f);
+            const bool bad = !(d < B);
+            const bool ti = !bad && f - fl == 0.5;
+            q[i] = bad ? 0ull : (u64)(ti ? fl : rint(f));
+            if (bad && lbad == SEG_E) lbad = i;
+            tie |= (unsigned)ti << i;
+            const unsigned qo = (unsigned)(q[i] & 1ull);
+            SegSum e;
+            if (ti) { e.f0 = 0u; e.f1 = 0u; e.T0 = q[i] + qo; e.T1 = q[i] + (qo ^ 1u); }
+            else { e.f0 = qo; e.f1 = qo ^ 1u; e.T0 = q[i]; e.T1 = q[i]; }
+            th = seg_then(th, e);
+        }
+        // inclusive scan of the thread segments over the wave
+        SegSum inc = th;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const SegSum y = seg_shfl_up(inc, o);
+            if (lane >= o) inc = seg_then(y, inc);
+        }
+        SegSum ex = seg_shfl_up(inc, 1);           // exclusive within the wave
+        if (lane == 0) ex = ident;
+        if (lane == 63) wagg[it][wave] = inc;
+        __syncthreads();
+        SegSum pre = ident, all = ident;
+#pragma unroll
+        for (int w2 = 0; w2 < NWV; ++w2) {
+            const SegSum a = wagg[it][w2];
+            if (w2 < wave) pre = seg_then(pre, a);
+            all = seg_then(all, a);
+        }
+        pre = seg_then(pre, ex);
+        // the thread's first step that changes the binade (P then holds the prefix before it)
+        const unsigned p0 = (unsigned)(base & 1ull);
+        unsigned p = p0 ? pre.f1 : pre.f0;
+        u64 P = p0 ? pre.T1 : pre.T0;
+        long long fb = LLONG_MAX;
+#pragma unroll
+        for (int i = 0; i < SEG_E; ++i) {
+            if (fb != LLONG_MAX) continue;
+            const unsigned qo = (unsigned)(q[i] & 1ull);
+            const bool ti = (tie >> i) & 1u;
+            const u64 d_inc = ti ? q[i] + (p ^ qo) : q[i];
+            if (i == lbad || base + P + d_inc >= top) {
+                fb = (long long)t * SEG_E + i;
+            } else {
+                P += d_inc;
+                p = ti ? 0u : (p ^ qo);
+            }
+        }
+        long long m = fb;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_xor(m, o);
+            m = y < m ? y : m;
+        }
+        if (lane == 0) wmin[it][wave] = m;
+        __syncthreads();
+        long long j = LLONG_MAX;
+#pragma unroll
+        for (int w2 = 0; w2 < NWV; ++w2) j = wmin[it][w2] < j ? wmin[it][w2] : j;
+        if (j == LLONG_MAX) {    // the whole chunk in one binade
+            s = ldexp((double)(base + (p0 ? all.T1 : all.T0)), -sh);
+            k0 += SEG_CH;
+        } else {                 // s at step j exactly, then step j as the reference adds it
+            if (fb == j) snext[it] = ldexp((double)(base + P), -sh) + v[k0 + j];
+            __syncthreads();
+            s = snext[it];
+            k0 += j + 1;
+        }
+    }
+    if (t == 0) *out = s;
+}
+
+// DM_SEQ_SUM=chain: the dependent-chain kernel (A/B)
 static void seq_sum(const double *d, long long n, double *out, hipStream_t st)
 {
-    k_seq_sum<<<1, 64, 0, st>>>(d, n, out);
+    const char *e = getenv("DM_SEQ_SUM");
+    if (e && !strcmp(e, "chain")) k_seq_sum<<<1, 64, 0, st>>>(d, n, out);
+    else k_seq_sum_seg<<<1, SEG_T, 0, st>>>(d, n, out);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -464,6 +620,19 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
 #undef DM_BILAT_PF
     PHIP_TRY(hipGetLastError());
     seq_sum(d_diff, n, d_error, st);
+    PHIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_seq_sum(const double *d_v, int64_t n, double *d_out, void *stream)
+{
+    if (n < 0 || (n > 0 && !d_v) || !d_out) return pfail(DM_ERR_ARG, "bad sequence sum arguments");
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) {
+        PHIP_TRY(hipMemsetAsync(d_out, 0, sizeof(double), st));
+        return DM_OK;
+    }
+    seq_sum(d_v, (long long)n, d_out, st);
     PHIP_TRY(hipGetLastError());
     return DM_OK;
 }

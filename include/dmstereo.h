@@ -248,14 +248,22 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
                           const int32_t *d_order, const int32_t *d_off, int32_t n_levels,
                           double *d_diff, double *d_error, void *stream);
 
+/* Sum of d_v[0..n) in sequence order, the float64 loop `error += v` of
+ * misc/optimize_loop.py:34 / misc/opt_loop.py:33 bit for bit, for terms >= 0 (NaN and inf
+ * propagate as in the loop).  Computed as exact integer prefix sums between the steps where
+ * the running sum climbs a binade or a tie occurs (dm_postproc.hip, k_seq_sum_seg).  *d_out
+ * (device) receives the sum; n == 0 gives +0.  The post-processing entries use it for their
+ * error sums. */
+int dm_seq_sum(const double *d_v, int64_t n, double *d_out, void *stream);
+
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 106 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 107 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
  * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
- * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256). */
+ * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus
