@@ -195,13 +195,15 @@ def volume_roofline(solver, reps=3, f16=False):
             'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
             'traffic': load_traffic(batch.h0, key, batch.T),
+            'store_pattern_ceiling': store_ceiling(batch.h0, batch.T, esz, gbs),
             'minmax_known': {
                 'what': 'the same volume, per-patch min/max already in the stats workspace (after '
                         'the level kernel, as Correlation_map()() then co_map): dm_corr_volume_ex '
                         'with DM_VOLUME_MINMAX_KNOWN skips the min/max sweep',
                 'ms': round(ms_k, 3), 'achieved': round(gbs_k, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(gbs_k / HBM_PEAK_GBS, 4),
-                'traffic': load_traffic(batch.h0, key + '_mm', batch.T)}}
+                'traffic': load_traffic(batch.h0, key + '_mm', batch.T),
+                'store_pattern_ceiling': store_ceiling(batch.h0, batch.T, esz, gbs_k)}}
 
 
 def fp16_flip_rate(solver, tiles=2):
@@ -271,6 +273,26 @@ def load_pmc(tile, kernel='level1', tiles=None):
 
 def load_traffic(tile, kernel='level1', tiles=None):
     return load_pmc(tile, kernel, tiles).get('hbm_bytes_per_launch')
+
+
+def store_ceiling(tile, tiles, esz, gbs):
+    """The rate the volume kernels' own store pattern allows with no arithmetic
+    (tools/store_probe.hip, profiles/store_probe.jsonl: the same volume, 16-B nontemporal
+    stores, 4 x 256 B per instruction into 4 patch maps advancing a row at a time) and the
+    fraction of it this run reached; None for shapes the probe did not run."""
+    name = 'c%d_f%d' % (3 if tile == 128 else 5, 8 * esz)
+    try:
+        with open(os.path.join(REPO, 'profiles', 'store_probe.jsonl')) as f:
+            rows = [json.loads(ln) for ln in f if ln.strip()]
+    except OSError:
+        return None
+    for r in rows:
+        if r.get('shape') == name and r.get('tiles') == tiles:
+            c = r['vol_nt']['gb_s']
+            return {'gb_s': c, 'frac': round(gbs / c, 4), 'best_pattern_gb_s': r['seq']['gb_s'],
+                    'source': 'profile: tools/store_probe.hip (profiles/store_probe.jsonl), pattern '
+                              '"vol_nt"; best_pattern = each wave streaming a contiguous slab'}
+    return None
 
 
 def level_roofline(solver, tile, l1_ms):
