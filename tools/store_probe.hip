@@ -30,8 +30,10 @@ __device__ __forceinline__ void st16(char *p, v4u v)
     else *(v4u *)p = v;
 }
 
-// one wave = 16 patches x all rows; RB image rows per store burst
-template <int RB, bool NT>
+// one wave = 16 patches x all rows; RB image rows per store burst; ROT: each workgroup starts
+// its row sweep at its own row ((block * 37) mod S) and wraps, so the workgroups of the chip
+// are at different offsets inside their maps at any moment
+template <int RB, bool NT, bool ROT = false>
 __global__ __launch_bounds__(512) void k_vol(char *vol, int S, int esz)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -50,11 +52,14 @@ __global__ __launch_bounds__(512) void k_vol(char *vol, int S, int esz)
     }
     const v4u v = {(unsigned)lane, 1u, 2u, 3u};
     const int per_row = (int)(rowb / 256);
-    for (int q0 = 0; q0 < S; q0 += RB)
+    const int off = ROT ? (int)((blockIdx.x * 37u) % (unsigned)S) & ~(RB - 1) : 0;
+    for (int q00 = 0; q00 < S; q00 += RB) {
+        const int q0 = (q00 + off) % S;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             for (int k = 0; k < RB; ++k)
                 for (int j = 0; j < per_row; ++j) st16<NT>(out[r] + (size_t)(q0 + k) * rowb + j * 256, v);
+    }
 }
 
 template <bool NT>
@@ -103,6 +108,8 @@ int main()
         run("seq_nt", [&] { k_seq<true><<<grid, 512>>>(vol, slab); });
         run("vol", [&] { k_vol<1, false><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("vol_nt", [&] { k_vol<1, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("vol_rot_nt", [&] { k_vol<1, true, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("vol_rot", [&] { k_vol<1, false, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("vol4", [&] { k_vol<4, false><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("vol4_nt", [&] { k_vol<4, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
         printf("}\n");
