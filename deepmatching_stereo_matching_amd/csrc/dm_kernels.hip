@@ -1158,7 +1158,8 @@ static bool mfma_bf16(const dm_tiles *b)
 // waves per workgroup of k_level1_mfq (and the window layout dm_corr_stats writes for it):
 // column group width GW = G/NW tiles of 16 windows per wave.  GW = 4 (two pooled columns per
 // lane: the left neighbour of the second is in the lane, level 2 pools in the lane) where the
-// width gives 2 or 4 such waves and the packed-y path applies; GW = 2 otherwise.  Same box,
+// width gives 1, 2 or 4 such waves and the packed-y path applies (one wave: two cell blocks per
+// workgroup, launch_mfq_t); GW = 2 otherwise.  Same box,
 // bit-identical (tools/kbench.py, profiles/r03k_*): C3 (S=128) 7.96 -> 7.72 ms with 2 waves of
 // GW = 4 instead of 4 waves of GW = 2 (137 VGPRs: 3 waves/SIMD instead of 5), C5 (S=256)
 // 549 -> 487 ms with 4 waves instead of 8.
@@ -1169,7 +1170,7 @@ static int mfq_nw(const dm_tiles *b)
     const char *gw = getenv("DM_MFQ_GW");   // A/B knob: 2 forces the GW = 2 layout
     const int cap = (e && e[0] == '4') ? 4 : (e && e[0] == '2') ? 2 : 8;
     const bool g4 = !(gw && gw[0] == '2') && b->ws * b->ws <= 25 && G % 4 == 0 &&
-                    (G / 4 == 2 || G / 4 == 4) && G / 4 <= cap;
+                    (G / 4 == 1 || G / 4 == 2 || G / 4 == 4) && G / 4 <= cap;
     if (g4) return G / 4;
     return G / 2 < cap ? G / 2 : cap;
 }
@@ -1341,6 +1342,15 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
 #define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
     // GW = 4 with 4 waves: 4 waves/SIMD register budget (5 spills)
     if (KS == 1 && GW == 4 && NW == 4) { k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    // GW = 4 with one wave per cell block (S = 64, C2): two cell blocks per workgroup share
+    // the pow tables (one-wave workgroups would hold 20 KB of LDS per wave: 2 waves/SIMD)
+    if (KS == 1 && GW == 4 && NW == 1) {
+        const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
+        if (((size_t)b->T * bpt) % 2) return fail(DM_ERR_UNSUPPORTED, "odd cell-block count");
+        k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
     // GW = 4 with 2 waves (C3): 20 KB of LDS (the exchange arrays in the pow tables' hole)
     // allow 8 workgroups per CU, so a 4 waves/SIMD register budget (<= 128 VGPRs)
     if (KS == 1 && GW == 4 && NW == 2) { k_level1_mfq<1, 4, 2, 4, L2F, YF, BF><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }

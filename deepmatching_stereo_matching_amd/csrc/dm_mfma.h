@@ -477,42 +477,55 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds
                  : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
 }
 
-// storage of k_level1_mfq's exchange arrays: its own LDS, or (H) the pow tables' g32 hole
-template <bool H, typename T>
+// storage of k_level1_mfq's exchange arrays: its own LDS, or (H) the pow tables' g32 hole at
+// byte offset OFF
+template <bool H, typename T, int OFF = 0>
 struct XchOwn {
     __attribute__((aligned(16))) T v;
     __device__ T &get(PowLds &) { return v; }
 };
-template <typename T>
-struct XchOwn<true, T> {
-    __device__ T &get(PowLds &p) { return *reinterpret_cast<T *>(&p.g32[128]); }
+template <typename T, int OFF>
+struct XchOwn<true, T, OFF> {
+    __device__ T &get(PowLds &p) { return *reinterpret_cast<T *>((char *)&p.g32[128] + OFF); }
 };
 
 // L1 may be null when L2F (level 1 then lives only on chip); L2 is written when L2F.
-template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false>
+// NB 2x2-cell blocks per workgroup (NB = 2 where one wave spans a whole tile row, S = 64):
+// waves sb * NWc .. sb * NWc + NWc - 1 split block sb's columns; the blocks share the pow
+// tables, which is what a workgroup of more than one wave buys there.
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false, int NB = 1>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
     constexpr bool EQ = KS == 1 && YF && !BF;    // window stats ride in the B tile (qs_of_frag)
+    static_assert(NW % NB == 0, "blocks split the waves evenly");
+    constexpr int NWc = NW / NB;                 // waves per cell block
+    constexpr int XS = NWc > 1 ? NWc + 1 : 1;    // exchange slots (unused with one wave per block)
+    constexpr int XW = NWc > 1 ? NWc : 1;
     __shared__ PowLds plds;
     // exchange arrays; they live in the pow tables' unused g32 rows when they fit (PowLds),
     // which keeps the C3 instance (2 waves per workgroup) at <= 20 KB of LDS: 8 workgroups,
     // 4 waves per SIMD
     struct Xch {
-        // [pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at
+        // [block][pair parity][row][slot][cell group][child]: slot w+1 = y of wave w at
         // q1 = 16*GW*(w+1)-1, slot 0 = -inf (no window left of column 0)
-        float xch[2][2][NW + 1][4][4];
+        float xch[NB][2][2][XS][4][4];
         double stash[L2F ? NW : 1][64];  // [wave][row slot * L2V + column]: level-2 pow inputs
-        double xch2[2][NW][4];           // [level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
+        double xch2[NB][2][XW][4];       // [block][level-1 row parity][wave][cell]: level 1 at v = 8*GW*(w+1)-1
+    };
+    struct Red {
+        float red[NB][2][NWc][16];       // per-wave partial min / max per patch row
     };
     constexpr bool HOLE = sizeof(Xch) <= G32_HOLE;
+    constexpr bool HOLE_R = HOLE && sizeof(Xch) + sizeof(Red) <= G32_HOLE;
     __shared__ XchOwn<HOLE, Xch> xown;
+    __shared__ XchOwn<HOLE_R, Red, (int)sizeof(Xch)> rown;
     Xch &X = xown.get(plds);
     auto &xch = X.xch;
     auto &stash = X.stash;
     auto &xch2 = X.xch2;
-    __shared__ float red[2][NW][16];   // per-wave partial min / max per patch row
-    __shared__ float4 cst[4][6];       // [cell][field][child]: a_p, lo, hi, rmin, den, rinv
+    auto &red = rown.get(plds).red;
+    __shared__ float4 cst[NB][4][6];   // [block][cell][field][child]: a_p, lo, hi, rmin, den, rinv
     // LATE: the next even row's fragments are loaded after the level-1 emission instead of
     // before it (12 fewer live VGPRs through the emission, less latency cover)
     constexpr bool LATE = L2F;
@@ -523,17 +536,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     __shared__ double stash2[L2F && GW == 2 ? NW : 1][L2F && GW == 2 ? 64 : 1];
     const int tid = threadIdx.x;
     pow_lds_fill(plds, tid, 64 * NW, HOLE);
-    if (tid < 64) (&xch[0][0][0][0][0])[(tid >> 4) * (NW + 1) * 16 + (tid & 15)] = -INFINITY;
+    if (NWc > 1 && tid < 64 * NB)
+        (&xch[tid >> 6][0][0][0][0][0])[((tid & 63) >> 4) * XS * 16 + (tid & 15)] = -INFINITY;
     __syncthreads();
 
-    constexpr int G = GW * NW;
+    constexpr int G = GW * NWc;
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // cell block of the workgroup and wave in it (NB == 1: block 0, as the compiler cannot see
+    // wave < NW)
+    const int sb = NB > 1 ? wave / NWc : 0, wc = NB > 1 ? wave % NWc : wave;
     const int c = lane & 15, grp = lane >> 4;
     const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
     const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
     const int nbj = w1 / 2, bpt = ((h0 / 2) / 2) * nbj; // 2x2-cell blocks per tile
-    const int t = blockIdx.x / bpt;                      // whole workgroup in range (grid exact)
-    const int I0 = 2 * ((blockIdx.x % bpt) / nbj), J0 = 2 * ((blockIdx.x % bpt) % nbj);
+    const int blk = blockIdx.x * NB + sb;
+    const int t = blk / bpt;                             // whole workgroup in range (grid exact)
+    const int I0 = 2 * ((blk % bpt) / nbj), J0 = 2 * ((blk % bpt) % nbj);
     const size_t tb = (size_t)t * P;
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
@@ -551,8 +569,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     const int ab = YF ? DM_YBIAS : 0;
     const dm_v4i acc0 = {ab, ab, ab, ab};
     const unsigned mant = mant_mask_vgpr();   // pow14_zf's mantissa mask, kept in a VGPR
-    const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
-    const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
+    const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wc * GW) * KS * 64;
+    const int2 *Qt = QS + ((size_t)t * h0 * G + wc * GW) * 16;
 
     // one image row of this wave's column group: GW tiles of B fragments + window stats.
     // Rows are software-pipelined in pairs: the next row's loads are in flight while the
@@ -611,24 +629,24 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
             mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
         }
-        if (c == 0) { red[0][wave][4 * grp + r] = mn[r]; red[1][wave][4 * grp + r] = mx[r]; }
+        if (c == 0) { red[sb][0][wc][4 * grp + r] = mn[r]; red[sb][1][wc][4 * grp + r] = mx[r]; }
     }
     __syncthreads();
     // per-patch normalisation constants {a_p, rmin, rmax - rmin, RN(1/(rmax - rmin))} of the
     // 16 patches -> LDS (read back at each level-1 row instead of holding 16 VGPRs)
     // r_of_y as one med3(y * a_p, lo, hi): NORMED [-1, 1] ([1, 1] for a constant patch,
     // a_p = 0: OpenCV's 1), CCOEFF unclamped
-    if (wave == 0 && c < 4) {
+    if (wc == 0 && c < 4) {
         const int r = c;
         const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
         const float ap = s.aP[tb + p];
-        float a = red[0][0][4 * grp + r], b = red[1][0][4 * grp + r];
+        float a = red[sb][0][0][4 * grp + r], b = red[sb][1][0][4 * grp + r];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) { a = fminf(a, red[0][w][4 * grp + r]); b = fmaxf(b, red[1][w][4 * grp + r]); }
+        for (int w = 1; w < NWc; ++w) { a = fminf(a, red[sb][0][w][4 * grp + r]); b = fmaxf(b, red[sb][1][w][4 * grp + r]); }
         const float rmn = r_of_y(a, ap, g.method), rmx = r_of_y(b, ap, g.method);
         const float den = __fsub_rn(rmx, rmn);
         const bool cc = g.method == DM_TM_CCOEFF;
-        float *f = (float *)&cst[grp][0];
+        float *f = (float *)&cst[sb][grp][0];
         f[0 * 4 + r] = ap;
         f[1 * 4 + r] = cc ? -INFINITY : (ap == 0.0f ? 1.0f : -1.0f);
         f[2 * 4 + r] = cc ? INFINITY : 1.0f;
@@ -645,7 +663,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     constexpr int M2 = M >= 2 ? M / 2 : 1;    // level-2 columns per lane (M == 1: even lanes)
     float Cprev[M][4];
     double Racc2[M2], Cprev2[M2], l1p[M];
-    double *Lrow = L1 ? L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wave : nullptr;
+    double *Lrow = L1 ? L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1 + 8 * GW * wc : nullptr;
     const int w2 = w0 / 4, P2 = (h0 / 4) * w2;
     double *L2row = L2F ? L2 + ((size_t)t * P2 + (size_t)(I0 / 2) * w2 + J0 / 2) * P2 : nullptr;
 
@@ -678,7 +696,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto level2_row = [&](int u, const double (&l1p)[M]) {
         const double lft = __shfl(l1p[M - 1], lane - 1);
         // column -1 is padding: the value itself stands in (cellmax_d)
-        const double left = c != 0 ? lft : (wave == 0 ? l1p[0] : xch2[u & 1][wave - 1][grp]);
+        const double left = c != 0 ? lft : (wc == 0 ? l1p[0] : xch2[sb][u & 1][wc - 1][grp]);
         double Cq[M2];
         if constexpr (M == 1) { // L2 column 4*GW*w + c/2 on even lanes
             const double right = __shfl(l1p[0], lane + 1);
@@ -735,7 +753,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (lane < (slot + 1) * L2V) {
                     const double l2 = pow14_k(stash[wave][lane], plds);
-                    L2row[(size_t)(u2 - slot + lane / L2V) * w2 + 4 * GW * wave + lane % L2V] = l2;
+                    L2row[(size_t)(u2 - slot + lane / L2V) * w2 + 4 * GW * wc + lane % L2V] = l2;
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -760,17 +778,18 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
         if constexpr (!LATE) load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
         pool_cols(fb, Cb, lb);
-        if (c == 15) {
+        if (NWc > 1 && c == 15) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { xch[k][0][wave + 1][grp][r] = la[r]; xch[k][1][wave + 1][grp][r] = lb[r]; }
-            if (L2F && u > 0) xch2[k ^ 1][wave][grp] = l1p[M - 1];
+            for (int r = 0; r < 4; ++r) { xch[sb][k][0][wc + 1][grp][r] = la[r]; xch[sb][k][1][wc + 1][grp][r] = lb[r]; }
+            if (L2F && u > 0) xch2[sb][k ^ 1][wc][grp] = l1p[M - 1];
         }
         __syncthreads();
         {
             // left neighbour of pooled column 0: lane c-1's last tile (DPP row_shr:1); lane
             // c == 0 keeps the DPP "old" operand = wave w-1's edge value (slot w; -inf for w = 0)
-            const float4 xa = *(const float4 *)&xch[k][0][wave][grp][0];
-            const float4 xb = *(const float4 *)&xch[k][1][wave][grp][0];
+            const float4 ninf = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            const float4 xa = NWc > 1 ? *(const float4 *)&xch[sb][k][0][wc][grp][0] : ninf;
+            const float4 xb = NWc > 1 ? *(const float4 *)&xch[sb][k][1][wc][grp][0] : ninf;
             const float oa[4] = {xa.x, xa.y, xa.z, xa.w}, ob[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -785,8 +804,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         // a constant child map (den == 0) makes its values NaN (0 * inf in the Markstein step,
         // the reference's 0/0): pow14_zf and pow14_q4 map NaN to NaN, so the sum and level 1
         // of its cell are NaN, as in the reference
-        const float4 kap = cst[grp][0], klo = cst[grp][1], khi = cst[grp][2], kmn = cst[grp][3],
-                     kden = cst[grp][4], kinv = cst[grp][5];
+        const float4 kap = cst[sb][grp][0], klo = cst[sb][grp][1], khi = cst[sb][grp][2], kmn = cst[sb][grp][3],
+                     kden = cst[sb][grp][4], kinv = cst[sb][grp][5];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             float R[4], x[4];
@@ -824,7 +843,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     }
     if constexpr (L2F) {
         const int u = h0 / 2 - 1;
-        if (c == 15) xch2[u & 1][wave][grp] = l1p[M - 1];
+        if (NWc > 1 && c == 15) xch2[sb][u & 1][wc][grp] = l1p[M - 1];
         __syncthreads();
         level2_row(u, l1p);
     }

@@ -22,6 +22,7 @@ import sys
 SHAPES = {  # shape -> (kernel prefix, f16 instantiation?, json name, tile, tiles)
     'l12_c3': ('k_level1_mfq', None, 'pmc_level1.json', 128, 64),
     'l12_c5': ('k_level1_mfq', None, 'pmc_level1_s256.json', 256, 256),
+    'l12_c2': ('k_level1_mfq', None, 'pmc_level1_s64.json', 64, 64),
     'v16_c3': ('k_volume_ls', True, 'pmc_volume_f16.json', 128, 64),
     'v16_c5': ('k_volume_ls', True, 'pmc_volume_f16_s256.json', 256, 8),
     'v32_c3': ('k_volume_ls', False, 'pmc_volume.json', 128, 64),

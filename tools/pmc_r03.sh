@@ -4,6 +4,7 @@
 # FETCH_SIZE and WRITE_SIZE (separate passes: TCC slots), for
 #   l12_c3   dm_corr_level12, C3 batch (64 tiles of S=128)          tools/kbench.py
 #   l12_c5   dm_corr_level12, C5 pair (256 tiles of S=256)          tools/kbench.py
+#   l12_c2   dm_corr_level12, C2 pair (64 tiles of S=64)            tools/kbench.py
 #   v16_c3   dm_corr_volume_f16, 64 tiles of S=128                  tools/vbench.py
 #   v16_c5   dm_corr_volume_f16, 8 tiles of S=256
 #   v32_c3   dm_corr_volume (float32), 64 tiles of S=128
@@ -22,6 +23,7 @@ for s in $SHAPES; do
   case $s in
     l12_c3) CMD="$REPO/tools/kbench.py --variants l12 --rounds 1 --tile 128 --grid 8" ;;
     l12_c5) CMD="$REPO/tools/kbench.py --variants l12 --rounds 1 --tile 256 --grid 16" ;;
+    l12_c2) CMD="$REPO/tools/kbench.py --variants l12 --rounds 1 --tile 64 --grid 8" ;;
     v16_c3) CMD="$REPO/tools/vbench.py --f16 --rounds 1 --tiles 64 --tile 128" ;;
     v16_c5) CMD="$REPO/tools/vbench.py --f16 --rounds 1 --tiles 8 --tile 256" ;;
     v32_c3) CMD="$REPO/tools/vbench.py --rounds 1 --tiles 64 --tile 128" ;;
