@@ -1340,20 +1340,35 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     }
     // register budget: 5 waves/SIMD (measured best for both variants on C3)
 #define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    // fused path: the min-max clamp as the Markstein step's clamp bit (norm_clamp in dm_mfma.h);
+    // DM_MFQ_CLAMP=0 (A/B knob) keeps the v_med3_f32 form
+    const char *ce = getenv("DM_MFQ_CLAMP");
+    const bool cl = L2F && !(ce && ce[0] == '0');
     // GW = 4 with 4 waves: 4 waves/SIMD register budget (5 spills)
-    if (KS == 1 && GW == 4 && NW == 4) { k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    if (KS == 1 && GW == 4 && NW == 4) {
+        if (cl) k_level1_mfq<1, 4, 4, 4, L2F, YF, BF, 1, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
     // GW = 4 with one wave per cell block (S = 64, C2): two cell blocks per workgroup share
     // the pow tables (one-wave workgroups would hold 20 KB of LDS per wave: 2 waves/SIMD)
     if (KS == 1 && GW == 4 && NW == 1) {
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % 2) return fail(DM_ERR_UNSUPPORTED, "odd cell-block count");
-        k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (cl) k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2, L2F><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
     // GW = 4 with 2 waves (C3): 20 KB of LDS (the exchange arrays in the pow tables' hole)
     // allow 8 workgroups per CU, so a 4 waves/SIMD register budget (<= 128 VGPRs)
-    if (KS == 1 && GW == 4 && NW == 2) { k_level1_mfq<1, 4, 2, 4, L2F, YF, BF><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
+    if (KS == 1 && GW == 4 && NW == 2) {
+        if (cl) k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 1, L2F><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        else k_level1_mfq<1, 4, 2, 4, L2F, YF, BF><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
     DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 2, 8)
     if constexpr (!YF) {
         DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4) DM_MQ(2, 2, 8)

@@ -477,6 +477,35 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds
                  : "=&s"(keep) : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff) : "memory");
 }
 
+// Normalisation with the clamp bit (k_level1_mfq<..., CL = true>, the fused level-1/level-2
+// path): x = (med3(R a_p, lo, hi) - rmin) / den becomes clamp01((R a_p - rmin) / den), the
+// quotient by norm_mk's Markstein steps (= RN(a / den), monotone in a), bit for bit:
+//  - r inside [lo, hi]: same operands; x in [0, 1] already (rmin <= r <= rmax, a <= den), so the
+//    clamp changes nothing.  CCOEFF (lo, hi = -inf, inf) is always this case.
+//  - R a_p > 1: r = 1 = rmax (max_q y >= R), so a = RN(rmax - rmin) = den and x = 1 exactly;
+//    unclamped a' >= den gives x' >= 1, clamped to 1.
+//  - R a_p < -1: r = -1 = rmin, a = +0, x = +0; unclamped a' < 0 gives x' < 0, clamped to +0.
+//  - den == 0 (a constant child map; also every a_p == 0 patch, where r == 1 throughout): the
+//    reference's values are NaN (0/0), but the hardware clamp maps NaN to 0 (dx10_clamp).  Every
+//    level-1 value of such a cell is NaN and every level-2 value of its block is NaN (each sums
+//    all four cells), so the kernel writes NaN there itself: level 2 when any of the block's 16
+//    patches is flat (block_has_flat), a stored level 1 when one of the cell's 4 is (cell_flat).
+// Saves the four v_med3_f32 (4 issue cycles each) per four pooled values.
+__device__ __forceinline__ dm_f2 pk_fma_clamp01(dm_f2 a, dm_f2 b, dm_f2 c)
+{
+    dm_f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ bool cell_flat(float4 den)
+{
+    return den.x == 0.0f || den.y == 0.0f || den.z == 0.0f || den.w == 0.0f;
+}
+__device__ __forceinline__ bool block_has_flat(const float4 (&cst)[4][6])
+{
+    return cell_flat(cst[0][4]) || cell_flat(cst[1][4]) || cell_flat(cst[2][4]) || cell_flat(cst[3][4]);
+}
+
 // storage of k_level1_mfq's exchange arrays: its own LDS, or (H) the pow tables' g32 hole at
 // byte offset OFF
 template <bool H, typename T, int OFF = 0>
@@ -493,12 +522,13 @@ struct XchOwn<true, T, OFF> {
 // NB 2x2-cell blocks per workgroup (NB = 2 where one wave spans a whole tile row, S = 64):
 // waves sb * NWc .. sb * NWc + NWc - 1 split block sb's columns; the blocks share the pow
 // tables, which is what a workgroup of more than one wave buys there.
-template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false, int NB = 1>
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false, int NB = 1, bool CL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
     constexpr bool EQ = KS == 1 && YF && !BF;    // window stats ride in the B tile (qs_of_frag)
     static_assert(NW % NB == 0, "blocks split the waves evenly");
+    static_assert(!CL || L2F, "clamp-bit normalisation: NaN cells are restored at the level-2 / level-1 stores");
     constexpr int NWc = NW / NB;                 // waves per cell block
     constexpr int XS = NWc > 1 ? NWc + 1 : 1;    // exchange slots (unused with one wave per block)
     constexpr int XW = NWc > 1 ? NWc : 1;
@@ -659,6 +689,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     __syncthreads();
 
     // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 [-> level 2] ----
+    // CL (norm_clamp): level 2 of a block with a flat patch is NaN (wave-uniform, an SGPR), as
+    // is a stored level 1 of a cell with a flat child (a lane mask); both set once
+    const bool bflat = CL && __builtin_amdgcn_readfirstlane((int)block_has_flat(cst[sb])) != 0;
+    const bool cflat = CL && L1 && cell_flat(cst[sb][grp][4]);
     constexpr int M = GW / 2;                 // pooled columns per lane: v = 8*GW*wave + M*c + m
     constexpr int M2 = M >= 2 ? M / 2 : 1;    // level-2 columns per lane (M == 1: even lanes)
     float Cprev[M][4];
@@ -752,7 +786,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (lane < (slot + 1) * L2V) {
-                    const double l2 = pow14_k(stash[wave][lane], plds);
+                    double l2 = pow14_k(stash[wave][lane], plds);
+                    if (CL && bflat) l2 = (double)NAN; // see norm_clamp
                     L2row[(size_t)(u2 - slot + lane / L2V) * w2 + 4 * GW * wc + lane % L2V] = l2;
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -760,6 +795,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
     };
 
+    // CL: a stored level 1 of a cell with a flat child is NaN (norm_clamp); a lane mask, set once
     // rows in pairs (q0 even, q0 + 1 odd) = level-1 row u = q0 / 2; one barrier per pair
     // publishes both rows' edge values and the previous pair's level-1 edge value
     for (int q0 = 0; q0 < h0; q0 += 2) {
@@ -804,8 +840,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         // a constant child map (den == 0) makes its values NaN (0 * inf in the Markstein step,
         // the reference's 0/0): pow14_zf and pow14_q4 map NaN to NaN, so the sum and level 1
         // of its cell are NaN, as in the reference
-        const float4 kap = cst[sb][grp][0], klo = cst[sb][grp][1], khi = cst[sb][grp][2], kmn = cst[sb][grp][3],
-                     kden = cst[sb][grp][4], kinv = cst[sb][grp][5];
+        const float4 kap = cst[sb][grp][0], kmn = cst[sb][grp][3], kden = cst[sb][grp][4], kinv = cst[sb][grp][5];
+        float4 klo = kap, khi = kap;
+        if constexpr (!CL) { klo = cst[sb][grp][1]; khi = cst[sb][grp][2]; }
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             float R[4], x[4];
@@ -814,16 +851,27 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                 R[r] = fmaxf(Ca[m][r], Cb[m][r]);
                 Cprev[m][r] = Cb[m][r];
             }
-            // r = med3(R * a_p, lo, hi); x = (r - rmin) / den (Markstein, see norm_mk), packed
+            // r = med3(R * a_p, lo, hi); x = (r - rmin) / den (Markstein, see norm_mk), packed.
+            // CL: the med3 is the clamp bit of the last Markstein step instead (see norm_clamp)
             const dm_f2 ra = dm_f2{R[0], R[1]} * dm_f2{kap.x, kap.y}, rb = dm_f2{R[2], R[3]} * dm_f2{kap.z, kap.w};
-            const float r4[4] = {__builtin_amdgcn_fmed3f(ra.x, klo.x, khi.x), __builtin_amdgcn_fmed3f(ra.y, klo.y, khi.y),
-                                 __builtin_amdgcn_fmed3f(rb.x, klo.z, khi.z), __builtin_amdgcn_fmed3f(rb.y, klo.w, khi.w)};
+            float r4[4] = {ra.x, ra.y, rb.x, rb.y};
+            if constexpr (!CL) {
+                r4[0] = __builtin_amdgcn_fmed3f(ra.x, klo.x, khi.x); r4[1] = __builtin_amdgcn_fmed3f(ra.y, klo.y, khi.y);
+                r4[2] = __builtin_amdgcn_fmed3f(rb.x, klo.z, khi.z); r4[3] = __builtin_amdgcn_fmed3f(rb.y, klo.w, khi.w);
+            }
             const dm_f2 a01 = dm_f2{r4[0], r4[1]} - dm_f2{kmn.x, kmn.y}, a23 = dm_f2{r4[2], r4[3]} - dm_f2{kmn.z, kmn.w};
             const dm_f2 i01 = {kinv.x, kinv.y}, i23 = {kinv.z, kinv.w};
             const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
             const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{kden.x, kden.y}, a01);
             const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{kden.z, kden.w}, a23);
-            const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01), x23 = __builtin_elementwise_fma(e23, i23, q23);
+            dm_f2 x01, x23;
+            if constexpr (CL) {
+                x01 = pk_fma_clamp01(e01, i01, q01);
+                x23 = pk_fma_clamp01(e23, i23, q23);
+            } else {
+                x01 = __builtin_elementwise_fma(e01, i01, q01);
+                x23 = __builtin_elementwise_fma(e23, i23, q23);
+            }
             x[0] = x01.x; x[1] = x01.y; x[2] = x23.x; x[3] = x23.y;
             double sum = 0.0;
 #pragma unroll
@@ -834,7 +882,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             // level 1 = pow14(sum / 4), rectified where it is read: here when level 1 is
             // stored, after level 2's MaxPool otherwise (see level2_row)
             l1p[m] = sum;
-            if (L1) Lrow[(size_t)u * w1 + M * c + m] = pow14_q4(sum, plds);
+            if (L1) Lrow[(size_t)u * w1 + M * c + m] = cflat ? (double)NAN : pow14_q4(sum, plds);
         }
         if constexpr (L2F) {
             if (u > 0) level2_row(u - 1, l1q);

@@ -308,22 +308,31 @@ def test_fused_level2_equals_aggregate(h0, w0, ws, method=5):
     _same(fused.level(1).cpu().numpy(), ref.levels[1].cpu().numpy())
 
 
-@pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (32, 128, 7)])
+@pytest.mark.parametrize('h0,w0,ws', [(64, 64, 5), (32, 128, 7), (128, 128, 5), (256, 256, 5)])
 def test_fused_level2_ccoeff_and_flat_patches(h0, w0, ws):
-    """The fused path with cv2.TM_CCOEFF, and with constant patches (NaN child maps)."""
-    test_fused_level2_equals_aggregate(h0, w0, ws, method=4)
+    """The fused path with cv2.TM_CCOEFF, and with constant patches (NaN child maps).  At
+    S = 64..256 the fused kernel normalises with the clamp bit and writes the NaN of flat
+    cells / blocks itself (norm_clamp in dm_mfma.h): level 1 (stored, mode 1) and level 2
+    must equal the unfused path's NaN pattern and values bit for bit."""
+    if h0 <= 128:
+        test_fused_level2_equals_aggregate(h0, w0, ws, method=4)
     from deepmatching_stereo_matching_amd import engine
     from deepmatching_stereo_matching_amd.synthetic import stereo_pair
     a, b = stereo_pair(h0 + ws - 1 + 4, w0 + ws - 1 + 8, seed=h0 + 3 * ws, dx=2)
     a[10:10 + ws + 3, 20:20 + ws + 5] = 200        # constant patches -> NaN maps (NORMED)
+    b[30:30 + ws + 2, 40:40 + ws + 9] = 90         # flat windows (dI == 0 -> 0)
     org = [(0, 0), (4, 8)]
     res = []
-    for mode in (0, 2):
+    for mode in (0, 1, 2):
         pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, h0, w0, ws, 5), fuse_level2=mode)
-        res.append((pyr.levels[2].cpu().numpy(), pyr.match().cpu().numpy()))
-    assert np.isnan(res[0][0]).any()
-    _same(res[0][0], res[1][0])
-    _same(res[0][1], res[1][1])
+        res.append((pyr.levels[2].cpu().numpy(), pyr.match().cpu().numpy(),
+                    None if pyr.levels[1] is None else pyr.levels[1].cpu().numpy()))
+    assert np.isnan(res[0][0]).any() and np.isnan(res[0][2]).any()
+    assert not np.isnan(res[0][0]).all()
+    for r in res[1:]:
+        _same(res[0][0], r[0])
+        _same(res[0][1], r[1])
+    _same(res[0][2], res[1][2])
 
 
 def test_fused_level2_unsupported_shapes():

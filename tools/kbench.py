@@ -40,7 +40,7 @@ def main():
             parts = v.split('+')
             fused = parts[0] == 'l12'       # dm_corr_level12 (level 2 fused, level 1 on chip)
             os.environ['DM_LEVEL1'] = 'mfq' if fused else parts[0]
-            for kv in ('DM_MF16_MINW', 'DM_MF16_PF', 'DM_MFQ_MINW', 'DM_MFQ_NWMAX', 'DM_MFQ_GW'):
+            for kv in ('DM_MF16_MINW', 'DM_MF16_PF', 'DM_MFQ_MINW', 'DM_MFQ_NWMAX', 'DM_MFQ_GW', 'DM_MFQ_CLAMP'):
                 os.environ.pop(kv, None)
             for kv in parts[1:]:
                 k, val = kv.split('=')
