@@ -28,6 +28,18 @@ __constant__ double c_powf_c[DM_POWF_NT] = DM_POWF_C_INIT;
 __constant__ double c_powf_p[DM_POWF_NT * 2] = DM_POWF_P_INIT;
 __constant__ double c_powf_g[(1 - DM_POWF_EMIN) * 2] = DM_POWF_G_INIT;
 
+// Kernels of a pair's tail (stats, levels >= 3, matching, sub-pixel, stitch) run beside the next
+// pair's level kernel, whose waves are older and win the SIMD's age-ordered issue arbitration on
+// nearly every cycle; a tail wave then waits for the few idle issue slots between its loads
+// and holds its wave slot ~20x longer than alone (profiles/r03y_gaps.txt).  With
+// DM_TAIL_PRIO, tail waves raise their priority (s_setprio) so their short, latency-bound
+// instruction streams issue as soon as they are ready.
+#ifdef DM_TAIL_PRIO
+#define DM_TAIL_ENTRY() __builtin_amdgcn_s_setprio(3)
+#else
+#define DM_TAIL_ENTRY() ((void)0)
+#endif
+
 __device__ __forceinline__ double pow14(double x)
 {
     if (x >= DM_POWF_XMIN && x <= 1.0) return dm_pow14_fast(x, c_powf_c, c_powf_p, c_powf_g);
@@ -256,6 +268,7 @@ __device__ __forceinline__ float r_of_y_fast(float y, float a, int method)
 // ------------------------------------------------------------------------------------
 __global__ void k_stats(Geo g, Stats s)
 {
+    DM_TAIL_ENTRY();
     const int P = g.h0 * g.w0;
     const int t = blockIdx.y;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -516,6 +529,7 @@ __device__ __forceinline__ double nanmax(double acc, double v) { return (v > acc
 
 __global__ void k_aggregate(const double *in, int T, int h, int w, int rectify, double *out)
 {
+    DM_TAIL_ENTRY();
     const int h2 = h / 2, w2 = w / 2;
     const size_t P = (size_t)h * w, P2 = (size_t)h2 * w2;
     const size_t total = (size_t)T * P2 * P2;
@@ -555,6 +569,7 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void k_aggregate_rows(const double *in, int T, int h, int w, int BR, int rectify,
                                                         double *out)
 {
+    DM_TAIL_ENTRY();
     extern __shared__ double pooled[]; // [child][band row][v]: 4 * BR * W2 doubles (dynamic, so
                                        // small bands do not cap the workgroups per CU)
     const int h2 = h / 2, W2 = w / 2;
@@ -651,6 +666,7 @@ __device__ __forceinline__ void window_lvl(const double *M, int h, int w, int pd
 // top of the pyramid (_initial_move_map, :80-96): p_dot = p
 __global__ void k_match_top(const double *LK, int T, int h, int w, double *map)
 {
+    DM_TAIL_ENTRY();
     const size_t P = (size_t)h * w;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
@@ -674,6 +690,7 @@ __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r
 __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, int h, int w,
                              const double *pmap, double *cmap)
 {
+    DM_TAIL_ENTRY();
     const int hn = 2 * h, wn = 2 * w;
     const size_t P = (size_t)h * w, Pn = (size_t)hn * wn;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -833,6 +850,7 @@ struct PatchL0 {
 template <int WS, int MW = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
 {
+    DM_TAIL_ENTRY();
     constexpr int ws = WS, n = WS * WS;
     const int h0 = g.h0, w0 = g.w0;
     const int h1 = h0 / 2, w1 = w0 / 2, h = h1 / 2, w = w1 / 2;
@@ -933,6 +951,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
 // rectified level 0 ([T][P][P]) or nullptr (on demand from images + stats).
 __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, double *map)
 {
+    DM_TAIL_ENTRY();
     const size_t P = (size_t)h0 * w0;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
@@ -968,6 +987,7 @@ __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0
 // mean / median of the neighbouring integer displacements.  in -> out (score copied).
 __global__ void k_filter(const double *in, double *out, int T, int h, int w, int fw, int median)
 {
+    DM_TAIL_ENTRY();
     const size_t P = (size_t)h * w;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
@@ -1010,6 +1030,7 @@ __global__ void k_filter(const double *in, double *out, int T, int h, int w, int
 
 __global__ void k_cal_map(const double *map, int T, int h, int w, int mode, double *out)
 {
+    DM_TAIL_ENTRY();
     const size_t P = (size_t)h * w;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
@@ -1053,6 +1074,7 @@ struct Modes {
 __global__ void k_stitch(const double *match, int n0, int n1, int h0, int w0, int s0, int s1,
                          Modes modes, int nmodes, double *dmap, double *score, int Hout, int Wout)
 {
+    DM_TAIL_ENTRY();
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)Hout * Wout) return;
     const int y = (int)(idx / Wout), x = (int)(idx % Wout);
@@ -1209,16 +1231,26 @@ static inline unsigned nblk(size_t n, unsigned bs)
 // DM_TAIL_MINW=6 (A/B knob): the ws = 5 on-demand matching kernels with a 6 waves/SIMD register
 // budget (<= 80 VGPRs), small enough to run beside a level kernel (3 waves of 144 VGPRs per
 // SIMD) instead of waiting for its workgroups to retire
-static bool tail_lean()
+static int tail_minw()
 {
     const char *e = getenv("DM_TAIL_MINW");
-    return e && e[0] == '6';
+    return (e && e[0] == '6') ? 6 : (e && e[0] == '4') ? 4 : 1;
+}
+// The ws = 5 on-demand matching kernels run in one-wave workgroups, which fit in the wave slot
+// a retiring level-kernel wave leaves (a 4-wave workgroup needs a free slot on every SIMD of a
+// CU at once): the pipelined C3 bench -0.35 % per pair, same box (profiles/r03z2_tail.txt).
+// DM_TAIL_WG=256 (A/B knob) restores 4-wave workgroups.
+static unsigned tail_wg()
+{
+    const char *e = getenv("DM_TAIL_WG");
+    return (e && e[0] == '2') ? 256u : 64u;
 }
 
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
 template <int WS, int MW = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
 {
+    DM_TAIL_ENTRY();
     const int hn = g.h0, wn = g.w0, h = hn / 2, w = wn / 2;
     const size_t Pp = (size_t)h * w, Pn = (size_t)hn * wn;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1262,6 +1294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
 template <int WS, int MW = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_subpix_t(Geo g, Stats s, int T, double *map)
 {
+    DM_TAIL_ENTRY();
     const int h0 = g.h0, w0 = g.w0;
     const size_t P = (size_t)h0 * w0;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1804,9 +1837,14 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l1<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l1<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: if (tail_lean()) k_match_step_l1<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                    else k_match_step_l1<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                    break;
+            case 5: {
+                const unsigned wg = tail_wg(), nbw = nblk(4 * n, wg);
+                const int mw = tail_minw();
+                if (mw == 6) k_match_step_l1<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                else if (mw == 4) k_match_step_l1<5, 4><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                else k_match_step_l1<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                break;
+            }
             case 7: k_match_step_l1<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l1<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l1<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1820,9 +1858,12 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l0<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l0<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: if (tail_lean()) k_match_step_l0<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                    else k_match_step_l0<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                    break;
+            case 5: {
+                const unsigned wg = tail_wg(), nbw = nblk(n, wg);
+                if (tail_minw() == 6) k_match_step_l0<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                else k_match_step_l0<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
+                break;
+            }
             case 7: k_match_step_l0<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l0<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l0<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1844,9 +1885,12 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_subpix_t<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 3: k_subpix_t<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
-            case 5: if (tail_lean()) k_subpix_t<5, 6><<<nb, 256, 0, st>>>(g, s, T, buf[cur]);
-                    else k_subpix_t<5><<<nb, 256, 0, st>>>(g, s, T, buf[cur]);
-                    break;
+            case 5: {
+                const unsigned wg = tail_wg(), nbw = nblk((size_t)T * h0 * w0, wg);
+                if (tail_minw() == 6) k_subpix_t<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur]);
+                else k_subpix_t<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur]);
+                break;
+            }
             case 7: k_subpix_t<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 9: k_subpix_t<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 11: k_subpix_t<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;

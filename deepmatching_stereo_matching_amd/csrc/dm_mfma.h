@@ -40,6 +40,7 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 template <int WSC>
 __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS, int bf)
 {
+    DM_TAIL_ENTRY();
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t total = (size_t)g.T * g.h0 * G * 16;
     if (idx >= total) return;
@@ -795,7 +796,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
     };
 
-    // CL: a stored level 1 of a cell with a flat child is NaN (norm_clamp); a lane mask, set once
     // rows in pairs (q0 even, q0 + 1 odd) = level-1 row u = q0 / 2; one barrier per pair
     // publishes both rows' edge values and the previous pair's level-1 edge value
     for (int q0 = 0; q0 < h0; q0 += 2) {
@@ -839,7 +839,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         // row pooling: even row q0 (Cprev already folded in) and odd row q0 + 1 close row u
         // a constant child map (den == 0) makes its values NaN (0 * inf in the Markstein step,
         // the reference's 0/0): pow14_zf and pow14_q4 map NaN to NaN, so the sum and level 1
-        // of its cell are NaN, as in the reference
+        // of its cell are NaN, as in the reference (CL: the clamp bit maps that NaN to 0, and
+        // the stores write the NaN instead -- bflat / cflat, norm_clamp)
         const float4 kap = cst[sb][grp][0], kmn = cst[sb][grp][3], kden = cst[sb][grp][4], kinv = cst[sb][grp][5];
         float4 klo = kap, khi = kap;
         if constexpr (!CL) { klo = cst[sb][grp][1]; khi = cst[sb][grp][2]; }
