@@ -145,7 +145,10 @@ class PairSolver:
         if timed:
             self.ev.append(ev)
         self.last_end = ev[1]
-        pyr.build(events=ev, wait=wait, nlev=self.levels, level_stream=level_stream)
+        diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
+        pyr.build(events=ev, wait=wait, nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
+        if diag:
+            return torch.zeros((self.batch.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
         return pyr.match(sub_pix=True, nlev=self.levels)
 
     def level1_ms(self):
