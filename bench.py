@@ -599,6 +599,10 @@ def main():
                           'pair_priority': args.pair_priority},
                'roofline': roof,
                'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
+        if os.environ.get('DM_BENCH_DIAG'):   # tools/run_r03dg.sh: skipped work, never a bench line
+            rec['metric'] = 'DIAGNOSTIC (not the metric): ' + rec['metric']
+            rec['diagnostic'] = ('DM_BENCH_DIAG=%s: matching (and, l12only, levels >= 3) skipped inside '
+                                 'the timed steps' % os.environ['DM_BENCH_DIAG'])
         if k_level:
             rec['k_level'] = k_level
         if out_hash:
