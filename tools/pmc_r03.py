@@ -28,6 +28,9 @@ SHAPES = {  # shape -> (kernel prefix, f16 instantiation?, json name, tile, tile
     'v32_c3': ('k_volume_ls', False, 'pmc_volume.json', 128, 64),
     'v16mm_c3': ('k_volume_ls', True, 'pmc_volume_f16_mm.json', 128, 64),
     'v32mm_c3': ('k_volume_ls', False, 'pmc_volume_mm.json', 128, 64),
+    'v32_c5': ('k_volume_ls', False, 'pmc_volume_s256.json', 256, 4),
+    'v16mm_c5': ('k_volume_ls', True, 'pmc_volume_f16_mm_s256.json', 256, 8),
+    'v32mm_c5': ('k_volume_ls', False, 'pmc_volume_mm_s256.json', 256, 4),
 }
 
 

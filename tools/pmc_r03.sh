@@ -9,6 +9,7 @@
 #   v16_c5   dm_corr_volume_f16, 8 tiles of S=256
 #   v32_c3   dm_corr_volume (float32), 64 tiles of S=128
 #   v16mm_c3, v32mm_c3   the same with the min/max known (dm_corr_volume_ex MINMAX_KNOWN)
+#   v32_c5, v16mm_c5, v32mm_c5   the C5 line's volumes (4 float32 / 8 binary16 tiles of S=256)
 # then tools/pmc_r03.py writes profiles/pmc_<kernel>[_s256].json.
 #   usage (GPU box): bash tools/pmc_r03.sh <tag> [shapes...]     -> gpurun_out/pmc3_<tag>/
 set -euo pipefail
@@ -28,6 +29,9 @@ for s in $SHAPES; do
     v16_c5) CMD="$REPO/tools/vbench.py --f16 --rounds 1 --tiles 8 --tile 256" ;;
     v32_c3) CMD="$REPO/tools/vbench.py --rounds 1 --tiles 64 --tile 128" ;;
     v16mm_c3) CMD="$REPO/tools/vbench.py --f16 --mm --rounds 1 --tiles 64 --tile 128" ;;
+    v32_c5) CMD="$REPO/tools/vbench.py --rounds 1 --tiles 4 --tile 256" ;;
+    v16mm_c5) CMD="$REPO/tools/vbench.py --f16 --mm --rounds 1 --tiles 8 --tile 256" ;;
+    v32mm_c5) CMD="$REPO/tools/vbench.py --mm --rounds 1 --tiles 4 --tile 256" ;;
     v32mm_c3) CMD="$REPO/tools/vbench.py --mm --rounds 1 --tiles 64 --tile 128" ;;
     *) echo "unknown shape $s"; exit 2 ;;
   esac

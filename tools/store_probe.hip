@@ -9,11 +9,12 @@
 // each with plain or nontemporal stores, 8 waves per workgroup as k_volume_ls.  No arithmetic:
 // the rate each pattern allows the write path.  One JSON line per shape on stdout.
 //   hipcc -O3 --offload-arch=gfx950 tools/store_probe.hip -o tools/store_probe.bin
-//   ./tools/store_probe.bin            (C3 binary16, C3 float32, C5 binary16 shapes)
+//   ./tools/store_probe.bin [shape...]  (c3_f16, c3_f32, c5_f16, c5_f32; default all)
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -72,12 +73,22 @@ __global__ __launch_bounds__(512) void k_seq(char *vol, size_t slab)
     for (size_t o = 0; o < slab; o += 1024) st16<NT>(base + o, v);
 }
 
-int main()
+int main(int argc, char **argv)
 {
     struct Shape { const char *name; int S, T, esz; };
-    const Shape shapes[] = {{"c3_f16", 128, 64, 2}, {"c3_f32", 128, 64, 4}, {"c5_f16", 256, 8, 2}};
+    const Shape all[] = {{"c3_f16", 128, 64, 2}, {"c3_f32", 128, 64, 4}, {"c5_f16", 256, 8, 2},
+                         {"c5_f32", 256, 4, 4}};
+    // argv: shape names to run (default: all)
+    Shape shapes[4];
+    int ns = 0;
+    for (const Shape &sh : all) {
+        bool want = argc < 2;
+        for (int i = 1; i < argc; ++i) want = want || strcmp(argv[i], sh.name) == 0;
+        if (want) shapes[ns++] = sh;
+    }
     size_t maxb = 0;
-    for (const Shape &sh : shapes) {
+    for (int i = 0; i < ns; ++i) {
+        const Shape &sh = shapes[i];
         const size_t b = (size_t)sh.T * sh.S * sh.S * sh.S * sh.S * sh.esz;
         maxb = b > maxb ? b : maxb;
     }
@@ -86,7 +97,8 @@ int main()
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (const Shape &sh : shapes) {
+    for (int i = 0; i < ns; ++i) {
+        const Shape &sh = shapes[i];
         const size_t P = (size_t)sh.S * sh.S, bytes = (size_t)sh.T * P * P * sh.esz;
         const unsigned grid = (unsigned)((size_t)sh.T * (sh.S / 4) * (sh.S / 4) / 8);
         const size_t slab = 16 * P * sh.esz;
