@@ -72,6 +72,9 @@ def parse():
                     help='1: the level kernels of all solves run on one stream of their own')
     ap.add_argument('--stats-stream', type=int, default=0,
                     help='1 (with --level-stream 1): stats of all solves on one stream of their own')
+    ap.add_argument('--chain-levels', type=int, default=1,
+                    help='1: each solve\'s level kernel waits for the previous one (no two level '
+                         'kernels on the GPU at once); 0: consecutive level kernels may overlap')
     ap.add_argument('--pair-priority', choices=('normal', 'high'), default='normal',
                     help='priority of the pair streams (stats, levels >= 3, matching, stitch)')
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c3',
@@ -502,7 +505,7 @@ def main():
         for s in solvers:
             st = streams[nsolve[0] % len(streams)]
             nsolve[0] += 1
-            wait = prev_end[0] if (st is not None and lstream is None) else None
+            wait = prev_end[0] if (st is not None and lstream is None and args.chain_levels) else None
             s.step(timed=timed, stream=st, wait=wait, level_stream=lstream, stats_stream=sstream)
             prev_end[0] = s.last_end
 
@@ -596,7 +599,7 @@ def main():
                           'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
                           'streams': nstreams, 'level_stream': bool(lstream is not None),
                           'stats_stream': bool(sstream is not None),
-                          'pair_priority': args.pair_priority},
+                          'pair_priority': args.pair_priority, 'chain_levels': bool(args.chain_levels)},
                'roofline': roof,
                'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
         if os.environ.get('DM_BENCH_DIAG'):   # tools/run_r03dg.sh: skipped work, never a bench line
