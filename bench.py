@@ -19,6 +19,11 @@ Timing is barrier + synchronize bracketed, max over ranks.  Consecutive pair sol
 pipelined over 2 HIP streams (--streams): a solve's level kernel waits for the previous
 solve's level kernel, and the previous pair's latency-bound tail (levels >= 3, matching,
 stitch) runs beside it; every step still solves its pair completely inside the timed region.
+Every timed solve's stitched maps are kept (on the device) and, after the timed region,
+compared bit for bit with the same pair solved again on one stream, un-pipelined
+(`step_outputs_identical`, `step_outputs`).  The default c3 line also carries `c5_split`:
+one 4096^2 pair per step with its 256 tiles split over the ranks and gathered to rank 0
+(north_star's 8-GPU target), with the N = 1 reference solved on rank 0 in the same run.
 
 Also reported: the roofline of the dominant kernel (dm_corr_level12), timed with HIP
 events on the launch stream inside the timed steps, the HBM roofline of the level-0
@@ -42,6 +47,9 @@ sys.path.insert(0, REPO)
 from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
 from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
+
+sys.path.insert(0, os.path.join(REPO, 'tools'))
+import kernel_hash  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 WS = 5
@@ -91,10 +99,15 @@ def parse():
                          'levels 0..k-1 only, as the reference Matching on co_map_list[:k] with '
                          'N_map = 2^(k-1); default: the full pyramid Correlation_map builds')
     ap.add_argument('--output-hash', action='store_true',
-                    help="after timing, solve once more and report sha256 of rank 0's stitched "
-                         "maps of its first pair (tests compare it across rank counts)")
+                    help="report sha256 of rank 0's stitched maps of its first pair, solved once "
+                         "more after timing (always reported with the step check)")
     ap.add_argument('--no-k-level', action='store_true',
                     help='skip the extra timed pass at BASELINE\'s k-level pyramid')
+    ap.add_argument('--no-step-check', action='store_true',
+                    help='do not keep the timed solves\' outputs for the bit-for-bit check after timing')
+    ap.add_argument('--no-c5-split', action='store_true',
+                    help='c3: skip the c5_split sub-line (one 4096^2 pair, tiles split over the ranks)')
+    ap.add_argument('--c5-steps', type=int, default=3, help='timed steps of the c5_split sub-line')
     return ap.parse_args()
 
 
@@ -277,8 +290,27 @@ def load_pmc(tile, kernel='level1', tiles=None):
     return {}
 
 
+def isa_check(d, key, kind, tile, esz=None):
+    """Does profile field `key` (an ISA hash recorded when the profile was made) name the kernel
+    bytes of the library this process loaded?  -> (ok, note)."""
+    sym = kernel_hash.symbol(kind, tile, esz)
+    cur = kernel_hash.kernel_hash(sym) if sym else None
+    rec = d.get(key)
+    if cur is None:
+        return False, 'no ISA hash for this kernel in the loaded library'
+    if rec != cur:
+        return False, ('stale profile: it was made on kernel ISA %s, the loaded library holds %s '
+                       '(re-run tools/pmc_r03.sh / tools/issue_model.py)' % (rec, cur))
+    return True, 'profile made on this build (kernel ISA %s)' % cur
+
+
 def load_traffic(tile, kernel='level1', tiles=None):
-    return load_pmc(tile, kernel, tiles).get('hbm_bytes_per_launch')
+    """PMC HBM bytes per launch of the committed profile -- None unless the profile was taken
+    on the kernel bytes this process loaded."""
+    d = load_pmc(tile, kernel, tiles)
+    esz = 2 if 'f16' in kernel else 4
+    ok, _ = isa_check(d, 'isa_sha16', 'level' if kernel == 'level1' else 'volume', tile, esz)
+    return d.get('hbm_bytes_per_launch') if ok else None
 
 
 def store_ceiling(tile, tiles, esz, gbs):
@@ -327,13 +359,18 @@ def level_roofline(solver, tile, l1_ms):
     peak = 1024 * SPEC_CLOCK_GHZ
     roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3),
             'unit': 'G SIMD-issue-cycles/s', 'peak': peak}
-    cyc = pmc.get('issue_cycles_per_launch')
+    # the issue model and the PMC counters are used only when they were made on the kernel
+    # bytes this process loaded (tools/kernel_hash.py); otherwise frac is null, with the reason
+    model_ok, model_note = isa_check(pmc, 'issue_model_isa_sha16', 'level', tile)
+    pmc_ok, pmc_note = isa_check(pmc, 'isa_sha16', 'level', tile)
+    roof['isa_check'] = {'issue_model': model_note, 'pmc': pmc_note}
+    cyc = pmc.get('issue_cycles_per_launch') if model_ok else None
     if cyc:
         achieved = cyc / (l1_ms * 1e-3) / 1e9
         roof.update({'achieved': round(achieved, 1), 'frac': round(achieved / peak, 4)})
         # the clock at which this live time would keep every SIMD issuing on every cycle
         roof['clock_ghz_at_full_issue'] = round(achieved / 1024, 4)
-        if pmc.get('gpu_cycles_per_launch'):
+        if pmc.get('gpu_cycles_per_launch') and pmc_ok:
             # the same model over the profiled launch's own cycles (GRBM_GUI_ACTIVE / 8 XCDs):
             # one run's time and clock, not this run's time with another run's clock
             roof['issue_occupancy_profiled'] = {
@@ -345,7 +382,10 @@ def level_roofline(solver, tile, l1_ms):
                           'peak': '1024 SIMDs x 2.4 GHz, MI355X_MICROARCH.md'}
     else:
         roof.update({'achieved': None, 'frac': None,
-                     'source': {'issue_cycles_per_launch': 'no issue model for this batch shape'}})
+                     'source': {'issue_cycles_per_launch': model_note if not model_ok and pmc
+                                else 'no issue model for this batch shape'}})
+    if not pmc_ok:
+        pmc = {}
     if pmc.get('valu_busy_frac'):
         roof['valu_busy_pmc'] = {'value': pmc['valu_busy_frac'], 'source': 'profile',
                                  'note': 'SQ_ACTIVE_INST_VALU x 4 over 1024 SIMDs x GRBM cycles: '
@@ -434,6 +474,170 @@ def make_pairs(args, tile, grid, rank, world):
     return pairs, idx, job_pairs
 
 
+class Pipeline:
+    """Consecutive pair solves over `nstreams` HIP streams, round-robin and pipelined: each
+    solve's level kernel waits for the previous solve's level kernel (chain_levels), so level
+    kernels never share the GPU with each other and each one's event time stays its own,
+    while the previous pair's latency-bound tail (levels >= 3, matching on demand, stitch:
+    ~5 % of a solve) runs beside it.  Each solve still solves its pair completely.  The c5
+    split's gather to rank 0 is issued from whichever stream the solve runs on: one process
+    group's collectives run in issue order on its own communication stream, each waiting for
+    the issuing stream, so solves on two streams gather in order."""
+
+    def __init__(self, solvers, dev, dist, nstreams=2, chain_levels=True, level_stream=False,
+                 stats_stream=False, priority=0):
+        self.solvers, self.dist, self.dev = solvers, dist, dev
+        self.chain = bool(chain_levels)
+        # level_stream: every solve's level kernel goes to one more stream (serialised there,
+        # no cross-pair event), so a pair's stats never wait behind the previous pair's tail.
+        # HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order: a stream
+        # sharing a queue with another waits behind that stream's work, so the pipeline keeps
+        # to 3 streams (1 pair stream + level + stats) or 4.
+        self.lstream = torch.cuda.Stream(device=dev) if level_stream else None
+        self.streams = ([torch.cuda.Stream(device=dev, priority=priority) for _ in range(nstreams)]
+                        if (nstreams > 1 or self.lstream is not None) else [None])
+        # stats_stream: every solve's stats + window operands on one more stream, ahead of it
+        self.sstream = (torch.cuda.Stream(device=dev) if (stats_stream and self.lstream is not None)
+                        else None)
+        self.nsolve = 0
+        self.prev_end = None
+
+    def step(self, timed=False, hold=None):
+        """One step: every solver's pair once.  hold: list that receives (solver index,
+        stitched (d_map, out_map)) of each solve, so its outputs can be checked after the
+        timed region (the tensors stay alive; nothing is copied inside it)."""
+        for i, s in enumerate(self.solvers):
+            st = self.streams[self.nsolve % len(self.streams)]
+            self.nsolve += 1
+            wait = self.prev_end if (st is not None and self.lstream is None and self.chain) else None
+            res = s.step(timed=timed, stream=st, wait=wait, level_stream=self.lstream,
+                         stats_stream=self.sstream)
+            self.prev_end = s.last_end
+            if hold is not None and res is not None:
+                hold.append((i, res))
+
+    def run(self, steps, warmup, timed=True, hold=None):
+        """warmup untimed steps, then `steps` timed ones bracketed by barrier + synchronize;
+        seconds, max over ranks"""
+        import torch.distributed as tdist
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize()
+        if self.dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step(timed=timed, hold=hold)
+        torch.cuda.synchronize()
+        if self.dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if self.dist:
+            t = torch.tensor([el], dtype=torch.float64, device=self.dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+
+def _bits(t):
+    """The raw bits of a float64 map (NaN-safe bitwise comparison: uncovered cells are NaN)."""
+    return t.contiguous().view(torch.int64)
+
+
+def _sha256(maps):
+    import hashlib
+    h = hashlib.sha256()
+    for t in maps:
+        h.update(t.cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+def check_step_outputs(held, solvers, dist, steps):
+    """Output check of the timed path.  Every solve of the timed steps -- pipelined over the
+    streams, level kernels event-chained or overlapped, buffers shared across streams through
+    record_stream -- left its stitched maps in `held`; each is compared bit for bit with the
+    same pair solved once more after timing, on one stream, un-pipelined (the path
+    tests/test_c3_batch.py pins tile by tile to the oracle).  The comparison runs on the
+    device; sha256 of pair 0's maps is taken for every step and for the re-solve.  With
+    ranks, `identical` is the AND over ranks (every rank takes part in the re-solve: the c5
+    split gathers)."""
+    torch.cuda.synchronize()
+    ref = [s.step() for s in solvers]            # current stream, no wait, no overlap
+    torch.cuda.synchronize()
+    bad = 0
+    for i, res in held:
+        if ref[i] is None or not all(torch.equal(_bits(a), _bits(b)) for a, b in zip(res, ref[i])):
+            bad += 1
+    step_hashes = [_sha256(res)[:16] for i, res in held if i == 0]
+    ref_hash = _sha256(ref[0]) if (ref and ref[0] is not None) else None
+    # a rank of the c5 split other than 0 receives no maps (held and ref empty): nothing to check
+    ok = int(bad == 0 and (len(held) > 0 or all(r is None for r in ref)))
+    if dist:
+        import torch.distributed as tdist
+        t = torch.tensor([ok], dtype=torch.int64, device=torch.cuda.current_device())
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
+        ok = int(t.item())
+    return {'identical': bool(ok), 'solves_checked': len(held), 'mismatched': bad,
+            'steps': steps, 'sha256': ref_hash, 'step_sha256_16': step_hashes,
+            'against': 'each timed solve\'s stitched (d_map, out_map) bit for bit vs the same pair '
+                       're-solved after timing on one stream, un-pipelined (rank 0\'s figures; '
+                       'identical = AND over ranks)'}
+
+
+def c5_split(args, rank, world, dev, dist):
+    """BASELINE configs[4] / north_star's "tiled 4096^2 pairs" line: one 4096^2 pair (16 x 16
+    tiles of S = 256, the reference's ImageCutSolver loop, image_cut_solver.py:144-179) per
+    step with its 256 tiles split over the ranks (rank r solves tiles r::N) and gathered to
+    rank 0 (RCCL over xGMI), which stitches.  Timed like the main line (warmup, barrier +
+    synchronize, max over ranks), outputs checked like it.  With N > 1, rank 0 then solves the
+    whole pair alone on its GPU (the other ranks wait at a barrier): the N = 1 reference of
+    the same run, so speedup = its ms_per_pair / the split's."""
+    import torch.distributed as tdist
+    tile, grid = CONFIGS['c5']
+    side = (grid + 1) * tile + WS - 1
+    a, b = stereo_pair(side, side, seed=1000, dx=2, max_disp=tile // 4, sinusoidal=True)
+    img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    del a, b
+    voxels = grid * grid * float(tile) ** 4
+    steps, warmup = args.c5_steps, 1
+    solver = PairSolver(img1, img2, tile, grid, split=world > 1)
+    pipe = Pipeline([solver], dev, dist, nstreams=max(1, args.streams), chain_levels=args.chain_levels)
+    held = [] if not args.no_step_check else None
+    el = pipe.run(steps, warmup, hold=held)
+    ms = el / steps * 1e3
+    out = {'workload': 'C5: one %dx%d pair per step, %dx%d tiles of S=%d, ws=%d, full pyramid + '
+                       'sub-pixel + cal_map + stitch; tiles split %d-way, gathered to rank 0'
+                       % (grid * tile, grid * tile, grid, grid, tile, WS, world),
+           'n_gpus': world, 'steps': steps, 'warmup': warmup, 'ms_per_pair': round(ms, 3),
+           'value': round(voxels / (ms * 1e-3) / 1e9, 3), 'unit': 'Gvox/s',
+           'level_kernel_ms': round(solver.level1_ms(), 3) if solver.ev else None}
+    if held is not None:
+        out['step_outputs'] = check_step_outputs(held, [solver], dist, steps)
+        del held
+    if world > 1:
+        out['split_breakdown'] = split_breakdown(solver, rank, world, dev)
+    del pipe, solver
+    torch.cuda.empty_cache()
+    ref_ms = ms
+    if world > 1:
+        if rank == 0:
+            alone = PairSolver(img1, img2, tile, grid, split=False)
+            p1 = Pipeline([alone], dev, False, nstreams=max(1, args.streams), chain_levels=args.chain_levels)
+            ref_ms = p1.run(steps, warmup) / steps * 1e3
+            del p1, alone
+            torch.cuda.empty_cache()
+        t = torch.tensor([ref_ms], dtype=torch.float64, device=dev)
+        tdist.broadcast(t, 0)
+        ref_ms = float(t.item())
+    out['reference_n1_ms_per_pair'] = round(ref_ms, 3)
+    out['speedup_vs_n1'] = round(ref_ms / ms, 3)
+    out['reference_n1'] = ('the same pair solved whole on rank 0\'s GPU alone in this run (same '
+                           'pipelining, steps and timing)' if world > 1 else 'this line (N = 1)')
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -466,7 +670,7 @@ def main():
     tile, grid = CONFIGS[args.config]
     tile, grid = args.tile or tile, args.grid or grid
     # c5 (BASELINE configs[4]): ONE pair per step, its tiles sharded over the ranks (strong
-    # scaling, results all-gathered); c4: a fixed batch of pairs split over the ranks
+    # scaling, results gathered to rank 0); c4: a fixed batch of pairs split over the ranks
     # (strong scaling); c2/c3: one pair per rank per step (weak scaling)
     split = args.config == 'c5' and world > 1
     host_pairs, pair_idx, job_pairs = make_pairs(args, tile, grid, rank, world)
@@ -478,66 +682,20 @@ def main():
     solver = solvers[0] if solvers else None
     voxels = grid * grid * float(tile) ** 4      # per pair
 
-    # --streams S: consecutive pair solves go to S HIP streams round-robin, pipelined: each
-    # solve's level kernel waits for the previous solve's level kernel (so level kernels never
-    # share the GPU with each other and each one's event time stays its own), while the
-    # previous pair's latency-bound tail (levels >= 3, matching on demand, stitch: ~5 % of a
-    # solve) runs beside it.  Each solve still solves its pair completely.  The c5 split's
-    # gather to rank 0 is issued from whichever stream the solve runs on: one process group's
-    # collectives run in issue order on its own communication stream, each waiting for the
-    # issuing stream, so solves on two streams gather in order.
     nstreams = max(1, args.streams)
-    prio = -1 if args.pair_priority == 'high' else 0
-    # --level-stream: every solve's level kernel goes to one more stream (serialised there,
-    # no cross-pair event), so a pair's stats never wait behind the previous pair's tail.
-    # HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order: a stream sharing a
-    # queue with another waits behind that stream's work, so the pipeline keeps to 3 streams
-    # (1 pair stream + level + stats) or 4.
-    lstream = torch.cuda.Stream(device=dev) if args.level_stream else None
-    streams = ([torch.cuda.Stream(device=dev, priority=prio) for _ in range(nstreams)]
-               if (nstreams > 1 or lstream is not None) else [None])
-    # --stats-stream: every solve's stats + window operands on one more stream, ahead of it
-    sstream = torch.cuda.Stream(device=dev) if (args.stats_stream and lstream is not None) else None
-    nsolve = [0]
-    prev_end = [None]
-
-    def step(timed=False):
-        for s in solvers:
-            st = streams[nsolve[0] % len(streams)]
-            nsolve[0] += 1
-            wait = prev_end[0] if (st is not None and lstream is None and args.chain_levels) else None
-            s.step(timed=timed, stream=st, wait=wait, level_stream=lstream, stats_stream=sstream)
-            prev_end[0] = s.last_end
-
-    def run(steps, warmup, timed=True):
-        """warmup untimed steps, then `steps` timed ones bracketed by barrier + synchronize;
-        seconds, max over ranks"""
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step(timed=timed)
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if dist:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
-
-    elapsed = run(args.steps, args.warmup)
+    pipe = Pipeline(solvers, dev, dist, nstreams=nstreams, chain_levels=args.chain_levels,
+                    level_stream=args.level_stream, stats_stream=args.stats_stream,
+                    priority=-1 if args.pair_priority == 'high' else 0)
+    held = [] if not args.no_step_check else None
+    elapsed = pipe.run(args.steps, args.warmup, hold=held)
     ms_step = elapsed / args.steps * 1e3
     value = job_pairs * args.steps * voxels / elapsed / 1e9
     l1_ms = solver.level1_ms() if solver else None
     if rank == 0 and solver is None:
         raise SystemExit('rank 0 has no pairs (--pairs < --gpus)')
+    # the timed solves' outputs, checked after the timed region
+    step_check = check_step_outputs(held, solvers, dist, args.steps) if held is not None else None
+    del held
 
     # BASELINE.json states C2 / C3 (/ C4) on a 3- / 4-level pyramid: the same timed run with
     # the pyramid cut to k levels (levels 0..k-1 built, matching starts at level k-1), next to
@@ -547,7 +705,7 @@ def main():
     if args.levels is None and k and not args.no_k_level and not split:
         for s_ in solvers:
             s_.levels = k
-        el_k = run(args.steps, 1, timed=False)
+        el_k = pipe.run(args.steps, 1, timed=False)
         for s_ in solvers:
             s_.levels = None
         k_level = {'levels': k, 'ms_per_step': round(el_k / args.steps * 1e3, 3),
@@ -557,16 +715,12 @@ def main():
                            'N_map = %d)' % (k, k, 2 ** (k - 1))}
 
     breakdown = split_breakdown(solver, rank, world, dev) if split else None
-    out_hash = None
-    if args.output_hash:
-        import hashlib
+    out_hash = step_check['sha256'] if step_check else None
+    if args.output_hash and out_hash is None:
         res = solvers[0].step() if solvers else None    # split: every rank takes part
         torch.cuda.synchronize()
         if res is not None:
-            h = hashlib.sha256()
-            for t in res:
-                h.update(t.cpu().numpy().tobytes())
-            out_hash = h.hexdigest()
+            out_hash = _sha256(res)
 
     if rank == 0:
         roof = level_roofline(solver, tile, l1_ms)
@@ -597,11 +751,14 @@ def main():
                           'window_size': WS, 'pyramid_levels': args.levels or 'full',
                           'pairs_per_step': job_pairs,
                           'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
-                          'streams': nstreams, 'level_stream': bool(lstream is not None),
-                          'stats_stream': bool(sstream is not None),
+                          'streams': nstreams, 'level_stream': bool(args.level_stream),
+                          'stats_stream': bool(args.stats_stream and args.level_stream),
                           'pair_priority': args.pair_priority, 'chain_levels': bool(args.chain_levels)},
                'roofline': roof,
                'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
+        if step_check is not None:
+            rec['step_outputs_identical'] = step_check['identical']
+            rec['step_outputs'] = step_check
         if os.environ.get('DM_BENCH_DIAG'):   # tools/run_r03dg.sh: skipped work, never a bench line
             rec['metric'] = 'DIAGNOSTIC (not the metric): ' + rec['metric']
             rec['diagnostic'] = ('DM_BENCH_DIAG=%s: matching (and, l12only, levels >= 3) skipped inside '
@@ -619,6 +776,16 @@ def main():
                 rec['fp16_flip_rate'] = fp16_flip_rate(solver)
         if world == 1 and not args.no_cpu_baseline and tile <= 128:   # S=256: 17 GB level 0 per tile on the host
             rec['cpu_baseline'] = cpu_baseline(args.cpu_sample_tiles, tile)
+
+    # north_star's "tiled 4096^2 pairs, 8 GPUs" line, carried by the default (c3) run, so the
+    # driver's `bench.py --gpus N` measures it at every N (all ranks take part)
+    if args.config == 'c3' and not args.no_c5_split and args.tile is None and args.grid is None:
+        del pipe
+        torch.cuda.empty_cache()
+        c5 = c5_split(args, rank, world, dev, dist)
+        if rank == 0:
+            rec['c5_split'] = c5
+    if rank == 0:
         print(json.dumps(rec))
     if dist:
         tdist.barrier()

@@ -1154,27 +1154,13 @@ static inline size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 static size_t base_stats_bytes(const dm_tiles *b) { return (size_t)6 * 4 * (size_t)b->T * b->h0 * b->w0; }
 
-// level-1 kernel variant: 2 = MFMA 16x16x64 (default where eligible), 0 = generic.
-// DM_LEVEL1=generic forces the generic kernel for A/B runs; it must not change between
-// dm_corr_stats and dm_corr_level1 of one batch (the window layout differs).
+// level-1 kernel variant, a function of the tile shape only (no environment, no state): 3 =
+// the column-split MFMA kernel k_level1_mfq where the shape allows it, 0 = the generic kernel.
+// dm_corr_stats lays the window operands out for the variant, and every later call on the same
+// batch re-derives the same decision from the same dm_tiles.
 static int level1_variant(const dm_tiles *b)
 {
-    const char *f = getenv("DM_LEVEL1");
-    if (f && strcmp(f, "generic") == 0) return 0;
-    if (!mf16_eligible(b)) return 0;
-    if (f && strcmp(f, "mf16") == 0) return 2;
-    return 3; // column-split k_level1_mfq
-}
-
-// bf16 MFMA operands for the column-split kernels (exact for ws <= 5: K = 32 >= n, integer
-// accumulators < 2^24, so no bias trick is needed).  Opt-in (DM_MFMA_BF16=1): on C3 it
-// measured even with the i8 MFMA (the kernels are not VALU-issue bound after the bias add
-// goes).  dm_corr_stats lays the window operands out accordingly; every consumer
-// re-derives the same decision.
-static bool mfma_bf16(const dm_tiles *b)
-{
-    const char *e = getenv("DM_MFMA_BF16");
-    return level1_variant(b) == 3 && b->ws <= 5 && e && e[0] == '1';
+    return mf16_eligible(b) ? 3 : 0;
 }
 
 // waves per workgroup of k_level1_mfq (and the window layout dm_corr_stats writes for it):
@@ -1188,13 +1174,9 @@ static bool mfma_bf16(const dm_tiles *b)
 static int mfq_nw(const dm_tiles *b)
 {
     const int G = b->w0 / 16;
-    const char *e = getenv("DM_MFQ_NWMAX"); // A/B knob: 2, 4 or 8 waves per workgroup at most
-    const char *gw = getenv("DM_MFQ_GW");   // A/B knob: 2 forces the GW = 2 layout
-    const int cap = (e && e[0] == '4') ? 4 : (e && e[0] == '2') ? 2 : 8;
-    const bool g4 = !(gw && gw[0] == '2') && b->ws * b->ws <= 25 && G % 4 == 0 &&
-                    (G / 4 == 1 || G / 4 == 2 || G / 4 == 4) && G / 4 <= cap;
+    const bool g4 = b->ws * b->ws <= 25 && G % 4 == 0 && (G / 4 == 1 || G / 4 == 2 || G / 4 == 4);
     if (g4) return G / 4;
-    return G / 2 < cap ? G / 2 : cap;
+    return G / 2 < 8 ? G / 2 : 8;
 }
 
 // second window region: the column-group layout of k_volume_ls (GW = 16 B of output per
@@ -1204,7 +1186,6 @@ static bool volume_ls_shape(const dm_tiles *b)   // sizes the workspace: no envi
     return mf16_eligible(b) && b->ws <= 5 && (b->h0 % 4) == 0 && ((size_t)(b->h0 / 4) * (b->w0 / 4)) % 8 == 0;
 }
 
-static bool volume_ls_eligible(const dm_tiles *b) { return volume_ls_shape(b) && !mfma_bf16(b); }
 
 static void mfma_views2(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
 {
@@ -1228,23 +1209,10 @@ static inline unsigned nblk(size_t n, unsigned bs)
     return (unsigned)(b > 0x7fffffff ? 0x7fffffff : b);
 }
 
-// DM_TAIL_MINW=6 (A/B knob): the ws = 5 on-demand matching kernels with a 6 waves/SIMD register
-// budget (<= 80 VGPRs), small enough to run beside a level kernel (3 waves of 144 VGPRs per
-// SIMD) instead of waiting for its workgroups to retire
-static int tail_minw()
-{
-    const char *e = getenv("DM_TAIL_MINW");
-    return (e && e[0] == '6') ? 6 : (e && e[0] == '4') ? 4 : 1;
-}
 // The ws = 5 on-demand matching kernels run in one-wave workgroups, which fit in the wave slot
 // a retiring level-kernel wave leaves (a 4-wave workgroup needs a free slot on every SIMD of a
 // CU at once): the pipelined C3 bench -0.35 % per pair, same box (profiles/r03z2_tail.txt).
-// DM_TAIL_WG=256 (A/B knob) restores 4-wave workgroups.
-static unsigned tail_wg()
-{
-    const char *e = getenv("DM_TAIL_WG");
-    return (e && e[0] == '2') ? 256u : 64u;
-}
+static constexpr unsigned TAIL_WG = 64u;
 
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
 template <int WS, int MW = 1>
@@ -1356,31 +1324,19 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
-template <bool L2F, bool YF, bool BF = false>
+template <bool L2F, bool YF>
 static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
                         hipStream_t st)
 {
     const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
     const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
     const Geo gg = make_geo(b);
-    const char *mw = getenv("DM_MFQ_MINW"); // A/B knob: register budget 4, 5 or 6 waves/SIMD
-    if (KS == 1 && GW == 2 && NW == 4 && mw && mw[0] >= '4' && mw[0] <= '6') {
-        if (mw[0] == '4') k_level1_mfq<1, 2, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else if (mw[0] == '5') k_level1_mfq<1, 2, 4, 5, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 2, 4, 6, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        HIP_TRY(hipGetLastError());
-        return DM_OK;
-    }
-    // register budget: 5 waves/SIMD (measured best for both variants on C3)
-#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF, BF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
-    // fused path: the min-max clamp as the Markstein step's clamp bit (norm_clamp in dm_mfma.h);
-    // DM_MFQ_CLAMP=0 (A/B knob) keeps the v_med3_f32 form
-    const char *ce = getenv("DM_MFQ_CLAMP");
-    const bool cl = L2F && !(ce && ce[0] == '0');
-    // GW = 4 with 4 waves: 4 waves/SIMD register budget (5 spills)
+    // the fused path (L2F) normalises with the clamp bit of the Markstein step (norm_clamp in
+    // dm_mfma.h); the level-1-only path keeps the v_med3_f32 form
+    constexpr bool CL = L2F;
+    // GW = 4 with 4 waves (S = 256, C5): 4 waves/SIMD register budget
     if (KS == 1 && GW == 4 && NW == 4) {
-        if (cl) k_level1_mfq<1, 4, 4, 4, L2F, YF, BF, 1, L2F><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 4, 4, 4, L2F, YF, BF><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        k_level1_mfq<1, 4, 4, 4, L2F, YF, 1, CL><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1389,30 +1345,30 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     if (KS == 1 && GW == 4 && NW == 1) {
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % 2) return fail(DM_ERR_UNSUPPORTED, "odd cell-block count");
-        if (cl) k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2, L2F><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 2><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        k_level1_mfq<1, 4, 2, 4, L2F, YF, 2, CL><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
     // GW = 4 with 2 waves (C3): 20 KB of LDS (the exchange arrays in the pow tables' hole)
     // allow 8 workgroups per CU, so a 4 waves/SIMD register budget (<= 128 VGPRs)
     if (KS == 1 && GW == 4 && NW == 2) {
-        if (cl) k_level1_mfq<1, 4, 2, 4, L2F, YF, BF, 1, L2F><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
-        else k_level1_mfq<1, 4, 2, 4, L2F, YF, BF><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        k_level1_mfq<1, 4, 2, 4, L2F, YF, 1, CL><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
+    // GW = 2 (ws > 5, or widths without a 4-tile split): register budget 5 waves/SIMD
+#define DM_MQ(KS_, GW_, NW_) if (KS == KS_ && GW == GW_ && NW == NW_) { k_level1_mfq<KS_, GW_, NW_, 5, L2F, YF><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, L1, L2); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_MQ(1, 2, 1) DM_MQ(1, 2, 2) DM_MQ(1, 2, 4) DM_MQ(1, 2, 8)
     if constexpr (!YF) {
-        DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 4, 4) DM_MQ(2, 2, 8)
-        DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 4, 4) DM_MQ(3, 2, 8)
-        DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 4, 4) DM_MQ(4, 2, 8)
+        DM_MQ(2, 2, 1) DM_MQ(2, 2, 2) DM_MQ(2, 2, 4) DM_MQ(2, 2, 8)
+        DM_MQ(3, 2, 1) DM_MQ(3, 2, 2) DM_MQ(3, 2, 4) DM_MQ(3, 2, 8)
+        DM_MQ(4, 2, 1) DM_MQ(4, 2, 2) DM_MQ(4, 2, 4) DM_MQ(4, 2, 8)
     }
 #undef DM_MQ
     return fail(DM_ERR_UNSUPPORTED, "no column-split instance for KS=%d GW=%d NW=%d", KS, GW, NW);
 }
 
-// packed-f32 y (YF) needs n <= 25 (see y_of_acc); DM_MFQ_YF=0 forces the integer path (A/B)
+// the packed-f32 y (YF) needs n <= 25 (see y_of_acc)
 template <bool L2F>
 static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, hipStream_t st)
 {
@@ -1420,26 +1376,18 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
     int2 *QS;
     mfma_views(b, d_stats, &Bw, &QS);
     const Stats s = stats_view(d_stats, b->T, b->h0 * b->w0);
-    const char *yf = getenv("DM_MFQ_YF");
-    if (mfma_bf16(b)) return launch_mfq_t<L2F, true, true>(b, s, Bw, QS, L1, L2, st);
-    if (b->ws <= 5 && !(yf && yf[0] == '0')) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st);
+    if (b->ws <= 5) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st);
     return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st);
 }
 
-// LDS-shared-window volume kernel (k_volume_ls) for the column-group layout (GW == 2, KS == 1,
-// i8 operands); DM_VOLUME_IMPL=cs selects the column-split kernel (A/B), DM_VOLUME_LSNW=8
-// eight waves (patch blocks) per workgroup, DM_VOLUME_NT=0 plain stores.
+// LDS-shared-window volume kernel (k_volume_ls): ws <= 5 on the MFMA shapes, 8 waves (patch
+// blocks) per workgroup, nontemporal stores
 template <typename OT>
 static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st,
                             int have_mm = 0)
 {
-    const char *impl = getenv("DM_VOLUME_IMPL");
-    if ((impl && impl[0] == 'c') || !volume_ls_eligible(b)) return DM_ERR_UNSUPPORTED;
-    const int G = b->w0 / 16;
-    const char *nwe = getenv("DM_VOLUME_LSNW"), *nte = getenv("DM_VOLUME_NT");
-    const int nw = (nwe && nwe[0] == '4') ? 4 : 8;
-    const bool nw4o5 = nwe && nwe[0] == '4' && nwe[1] == '5';   // "45": 4 waves, 5 waves/SIMD budget
-    const bool nt = !(nte && nte[0] == '0');
+    if (!volume_ls_shape(b)) return DM_ERR_UNSUPPORTED;
+    const int G = b->w0 / 16, nw = 8;
     const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
     if (bpt % nw) return DM_ERR_UNSUPPORTED;
     // the window operands in k_volume_ls's layout, in the second window region
@@ -1448,20 +1396,34 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     mfma_views2(b, d_stats, &Bw, &QS);
     const size_t n = (size_t)b->T * b->h0 * G * 16;
     const int GW = (int)(16 / sizeof(OT)) < G ? (int)(16 / sizeof(OT)) : G;   // = k_volume_ls's GW
-    if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
-    else k_prep_windows16<0><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS, 0);
+    if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS);
+    else k_prep_windows16<0><<<nblk(n, 256), 256, 0, st>>>(make_geo(b), G, GW, 1, Bw, QS);
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
-    if (nw4o5 && G == 8 && nt) {
-        k_volume_ls<8, 4, true, OT, 5><<<grid, 256, 0, st>>>(gg, s, Bw, QS, out, have_mm);
-        HIP_TRY(hipGetLastError());
-        return DM_OK;
-    }
-#define DM_VL(G_, NW_, NT_) if (G == G_ && nw == NW_ && nt == NT_) { k_volume_ls<G_, NW_, NT_, OT><<<grid, 64 * NW_, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
-    DM_VL(2, 8, true) DM_VL(4, 8, true) DM_VL(8, 8, true) DM_VL(16, 8, true)
-    DM_VL(8, 4, true) DM_VL(16, 4, true) DM_VL(8, 8, false) DM_VL(16, 8, false)
+#define DM_VL(G_) if (G == G_) { k_volume_ls<G_, 8, true, OT><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_VL(2) DM_VL(4) DM_VL(8) DM_VL(16)
 #undef DM_VL
+    return DM_ERR_UNSUPPORTED;
+}
+
+// the MFMA volume for the shapes k_volume_ls does not take (ws > 5; GW = 2 there): integer y,
+// nontemporal stores, a row staged in LDS where 16 x w0 floats fit
+template <typename OT>
+static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st)
+{
+    dm_v4i *Bw;
+    int2 *QS;
+    mfma_views(b, d_stats, &Bw, &QS);
+    const int KS = (b->ws * b->ws + 63) / 64, GW = b->w0 / 16 / mfq_nw(b);
+    const size_t waves = (size_t)b->T * (b->h0 / 4) * (b->w0 / 4);
+    const unsigned vgrid = (unsigned)((waves + 3) / 4);
+    const bool lds = b->w0 <= 128;
+    const Geo gg = make_geo(b);
+#define DM_VQ(KS_, LS_) if (KS == KS_ && GW == 2 && lds == LS_) { k_volume_mfq<KS_, 2, false, true, LS_, OT><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, out); HIP_TRY(hipGetLastError()); return DM_OK; }
+    DM_VQ(1, true) DM_VQ(1, false) DM_VQ(2, true) DM_VQ(2, false)
+    DM_VQ(3, true) DM_VQ(3, false) DM_VQ(4, true) DM_VQ(4, false)
+#undef DM_VQ
     return DM_ERR_UNSUPPORTED;
 }
 
@@ -1497,10 +1459,9 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         mfma_views(b, d_stats, &Bw, &QS);
         const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
         const size_t n = (size_t)b->T * b->h0 * G * 16;
-        const int GW = var == 3 ? G / mfq_nw(b) : G;
-        const int bf = mfma_bf16(b) ? 1 : 0;
-        if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS, bf);
-        else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS, bf);
+        const int GW = G / mfq_nw(b);
+        if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
+        else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
         HIP_TRY(hipGetLastError());
     }
     return DM_OK;
@@ -1518,33 +1479,6 @@ int dm_corr_level1(const dm_tiles *b, void *d_stats, double *d_level1, void *str
     hipStream_t st = (hipStream_t)stream;
     const int var = level1_variant(b);
     if (var == 3) return launch_mfq<false>(b, d_stats, d_level1, nullptr, st);
-    if (var == 2) {
-        dm_v4i *Bw;
-        int2 *QS;
-        mfma_views(b, d_stats, &Bw, &QS);
-        const int KS = (b->ws * b->ws + 63) / 64, G = b->w0 / 16;
-        const int waves = b->T * (b->h0 / 4) * (b->w0 / 4);
-        const unsigned grid = (unsigned)((waves + MF_WAVES - 1) / MF_WAVES);
-        const Geo gg = make_geo(b);
-        // A/B knobs (DM_MF16_MINW=3|4 waves per SIMD, DM_MF16_PF=0|1 tile prefetch) for the
-        // C3 shape; every other shape runs the default instance
-        const char *mw = getenv("DM_MF16_MINW"), *pf = getenv("DM_MF16_PF");
-        const int minw = (mw && mw[0] == '3') ? 3 : 4, pref = (pf && pf[0] == '1') ? 1 : 0;
-        if (KS == 1 && G == 8 && (minw != 4 || pref)) {
-            if (minw == 3 && pref) k_level1_mf16<1, 8, 3, true><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
-            else if (minw == 3) k_level1_mf16<1, 8, 3, false><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
-            else k_level1_mf16<1, 8, 4, true><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1);
-            HIP_TRY(hipGetLastError());
-            return DM_OK;
-        }
-#define DM_MF(KS_, G_) if (KS == KS_ && G == G_) { k_level1_mf16<KS_, G_, 4, false><<<grid, 64 * MF_WAVES, 0, st>>>(gg, s, Bw, QS, d_level1); HIP_TRY(hipGetLastError()); return DM_OK; }
-        DM_MF(1, 2) DM_MF(1, 4) DM_MF(1, 8) DM_MF(1, 16)
-        DM_MF(2, 2) DM_MF(2, 4) DM_MF(2, 8) DM_MF(2, 16)
-        DM_MF(3, 2) DM_MF(3, 4) DM_MF(3, 8) DM_MF(3, 16)
-        DM_MF(4, 2) DM_MF(4, 4) DM_MF(4, 8) DM_MF(4, 16)
-#undef DM_MF
-        return fail(DM_ERR_UNSUPPORTED, "no MFMA16 instance for KS=%d G=%d", KS, G);
-    }
     if (P > DM_GENERIC_MAX_P || k2_lds_bytes(b->h0, b->w0, b->ws) > 160 * 1024)
         return fail(DM_ERR_UNSUPPORTED, "tile too large for the generic level-1 kernel (P=%d)", P);
     switch (b->ws) {
@@ -1579,63 +1513,11 @@ static int volume_f32(const dm_tiles *b, void *d_stats, float *d_l0, void *strea
     const int P = b->h0 * b->w0;
     Stats s = stats_view(d_stats, b->T, P);
     dim3 grid(P, b->T);
-    if (level1_variant(b) == 3) { // MFMA path (the column-group window layout of dm_corr_stats)
-        dm_v4i *Bw;
-        int2 *QS;
-        mfma_views(b, d_stats, &Bw, &QS);
-        if (launch_volume_ls<float>(b, d_stats, s, d_l0, (hipStream_t)stream, have_mm) == DM_OK) return DM_OK;
-        const char *cs = getenv("DM_VOLUME_CS");
-        const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
-        const bool bf = mfma_bf16(b);
-        if (!(cs && cs[0] == '0') && b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
-            // column-split workgroups with a shared LDS stage (RB rows per store burst)
-            const unsigned cgrid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
-            const Geo gc = make_geo(b);
-            hipStream_t sc = (hipStream_t)stream;
-            const char *rbe = getenv("DM_VOLUME_RB"); // A/B knob: rows per store burst (C3 shape)
-            const int rb = rbe ? atoi(rbe) : 2;
-            const char *vm = getenv("DM_VOLUME_MINW");
-            if (bf) {
-                if (NW1 == 4) k_volume_cs<1, 2, 4, 2, true, 1, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, true><<<cgrid, 512, 0, sc>>>(gc, s, Bw, QS, d_l0);
-                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, true><<<cgrid, 128, 0, sc>>>(gc, s, Bw, QS, d_l0);
-                else k_volume_cs<1, 2, 1, 4, true, 1, true><<<cgrid, 64, 0, sc>>>(gc, s, Bw, QS, d_l0);
-                HIP_TRY(hipGetLastError());
-                return DM_OK;
-            }
-            if (NW1 == 4 && vm && vm[0] == '5') k_volume_cs<1, 2, 4, 4, true, 5><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 4 && vm && vm[0] == '6') k_volume_cs<1, 2, 4, 2, true, 6><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 4 && rb == 2) k_volume_cs<1, 2, 4, 2, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 4 && rb == 8) k_volume_cs<1, 2, 4, 8, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true><<<cgrid, 256, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true><<<cgrid, 512, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true><<<cgrid, 128, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            else k_volume_cs<1, 2, 1, 4, true><<<cgrid, 64, 0, sc>>>(gc, s, Bw, QS, d_l0);
-            HIP_TRY(hipGetLastError());
-            return DM_OK;
-        }
-        const int KS = (b->ws * b->ws + 63) / 64, GW = b->w0 / 16 / mfq_nw(b);
-        const size_t waves = (size_t)b->T * (b->h0 / 4) * (b->w0 / 4);
-        const unsigned vgrid = (unsigned)((waves + 3) / 4);
-        const char *nt = getenv("DM_VOLUME_NT"), *ls = getenv("DM_VOLUME_LS");
-        const bool ntst = !(nt && nt[0] == '0');
-        const bool lds = !(ls && ls[0] == '0') && b->w0 <= 128; // stage: 16 x w0 floats per wave
-        const bool yf = b->ws <= 5;
-        const Geo gg = make_geo(b);
-        hipStream_t st = (hipStream_t)stream;
-        if (bf) { // window operands are bf16 (KS = 1, GW = 2 or 4)
-            if (GW == 2 && lds) k_volume_mfq<1, 2, true, true, true, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
-            else if (GW == 2) k_volume_mfq<1, 2, true, true, false, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
-            else k_volume_mfq<1, 4, true, true, false, true><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0);
-            HIP_TRY(hipGetLastError());
-            return DM_OK;
-        }
-#define DM_VQ(KS_, GW_, YF_, NT_, LS_) if (KS == KS_ && GW == GW_ && yf == YF_ && ntst == NT_ && lds == LS_) { k_volume_mfq<KS_, GW_, YF_, NT_, LS_><<<vgrid, 256, 0, st>>>(gg, s, Bw, QS, d_l0); HIP_TRY(hipGetLastError()); return DM_OK; }
-        DM_VQ(1, 2, true, true, true) DM_VQ(1, 2, true, true, false) DM_VQ(1, 2, true, false, true) DM_VQ(1, 2, true, false, false)
-        DM_VQ(1, 4, true, true, false) DM_VQ(1, 4, true, false, false)
-        DM_VQ(1, 2, false, true, true) DM_VQ(1, 4, false, true, false) DM_VQ(2, 2, false, true, true) DM_VQ(2, 4, false, true, false)
-        DM_VQ(3, 2, false, true, true) DM_VQ(3, 4, false, true, false) DM_VQ(4, 2, false, true, true) DM_VQ(4, 4, false, true, false)
-#undef DM_VQ
+    if (level1_variant(b) == 3) { // MFMA paths (the window layouts of dm_corr_stats / k_volume_ls)
+        rc = launch_volume_ls<float>(b, d_stats, s, d_l0, (hipStream_t)stream, have_mm);
+        if (rc != DM_ERR_UNSUPPORTED) return rc;
+        rc = launch_volume_mfq<float>(b, d_stats, s, d_l0, (hipStream_t)stream);
+        if (rc != DM_ERR_UNSUPPORTED) return rc;
     }
     k_minmax<<<grid, 256, 0, (hipStream_t)stream>>>(make_geo(b), s);
     HIP_TRY(hipGetLastError());
@@ -1654,34 +1536,10 @@ static int volume_f16(const dm_tiles *b, void *d_stats, uint16_t *d_l0, void *st
     _Float16 *out = (_Float16 *)d_l0;
     hipStream_t st = (hipStream_t)stream;
     if (level1_variant(b) == 3) {
-        dm_v4i *Bw;
-        int2 *QS;
-        mfma_views(b, d_stats, &Bw, &QS);
-        if (launch_volume_ls<_Float16>(b, d_stats, s, out, st, have_mm) == DM_OK) return DM_OK;
-        const int KS1 = (b->ws * b->ws + 63) / 64, NW1 = mfq_nw(b), GW1 = b->w0 / 16 / NW1;
-        if (b->ws <= 5 && KS1 == 1 && GW1 == 2 && (b->h0 % 4) == 0) {
-            // the float32 column-split kernel with a binary16 stage: 4 rows per store burst
-            // keep the per-patch runs at RB*w0*2 = 1 KB (C3 shape)
-            const unsigned cgrid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
-            const Geo gc = make_geo(b);
-            if (mfma_bf16(b)) {
-                if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, true, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, true, _Float16><<<cgrid, 512, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, true, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
-                else k_volume_cs<1, 2, 1, 4, true, 1, true, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);
-            } else {
-                const char *vm = getenv("DM_VOLUME_MINW"); // A/B knob: waves per SIMD floor
-                if (NW1 == 4 && vm && vm[0] == '5') k_volume_cs<1, 2, 4, 4, true, 5, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 4 && vm && vm[0] == '6') k_volume_cs<1, 2, 4, 2, true, 6, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 4 && vm && vm[0] == '7') k_volume_cs<1, 2, 4, 4, true, 6, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 4) k_volume_cs<1, 2, 4, 4, true, 1, false, _Float16><<<cgrid, 256, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 8) k_volume_cs<1, 2, 8, 2, true, 1, false, _Float16><<<cgrid, 512, 0, st>>>(gc, s, Bw, QS, out);
-                else if (NW1 == 2) k_volume_cs<1, 2, 2, 4, true, 1, false, _Float16><<<cgrid, 128, 0, st>>>(gc, s, Bw, QS, out);
-                else k_volume_cs<1, 2, 1, 4, true, 1, false, _Float16><<<cgrid, 64, 0, st>>>(gc, s, Bw, QS, out);
-            }
-            HIP_TRY(hipGetLastError());
-            return DM_OK;
-        }
+        rc = launch_volume_ls<_Float16>(b, d_stats, s, out, st, have_mm);
+        if (rc != DM_ERR_UNSUPPORTED) return rc;
+        rc = launch_volume_mfq<_Float16>(b, d_stats, s, out, st);
+        if (rc != DM_ERR_UNSUPPORTED) return rc;
     }
     dim3 grid(P, b->T);
     k_minmax<<<grid, 256, 0, st>>>(make_geo(b), s);
@@ -1837,14 +1695,7 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l1<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l1<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: {
-                const unsigned wg = tail_wg(), nbw = nblk(4 * n, wg);
-                const int mw = tail_minw();
-                if (mw == 6) k_match_step_l1<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                else if (mw == 4) k_match_step_l1<5, 4><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                else k_match_step_l1<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                break;
-            }
+            case 5: k_match_step_l1<5><<<nblk(4 * n, TAIL_WG), TAIL_WG, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 7: k_match_step_l1<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l1<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l1<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1858,12 +1709,7 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_match_step_l0<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 3: k_match_step_l0<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
-            case 5: {
-                const unsigned wg = tail_wg(), nbw = nblk(n, wg);
-                if (tail_minw() == 6) k_match_step_l0<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                else k_match_step_l0<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]);
-                break;
-            }
+            case 5: k_match_step_l0<5><<<nblk(n, TAIL_WG), TAIL_WG, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 7: k_match_step_l0<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 9: k_match_step_l0<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
             case 11: k_match_step_l0<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur], buf[cur ^ 1]); break;
@@ -1885,12 +1731,7 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             switch (g.ws) {
             case 1: k_subpix_t<1><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 3: k_subpix_t<3><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
-            case 5: {
-                const unsigned wg = tail_wg(), nbw = nblk((size_t)T * h0 * w0, wg);
-                if (tail_minw() == 6) k_subpix_t<5, 6><<<nbw, wg, 0, st>>>(g, s, T, buf[cur]);
-                else k_subpix_t<5><<<nbw, wg, 0, st>>>(g, s, T, buf[cur]);
-                break;
-            }
+            case 5: k_subpix_t<5><<<nblk((size_t)T * h0 * w0, TAIL_WG), TAIL_WG, 0, st>>>(g, s, T, buf[cur]); break;
             case 7: k_subpix_t<7><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 9: k_subpix_t<9><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             case 11: k_subpix_t<11><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;

@@ -16,8 +16,6 @@
 typedef int dm_v4i __attribute__((ext_vector_type(4)));
 typedef int dm_v2i __attribute__((ext_vector_type(2)));
 
-#define MF_WAVES 4
-
 // ===================================================================================
 // 16x16x64 variant (default).  v_mfma_i32_16x16x64_i8: lane L holds A[row L&15][k = 64ks +
 // 16(L>>4) + j] and B[k][col L&15]; acc[reg] = C[row 4(L>>4) + reg][col L&15].
@@ -33,12 +31,12 @@ typedef int dm_v2i __attribute__((ext_vector_type(2)));
 // bytes 0..7 and the window's {qx, qy} in words 2, 3 (build_a places A's taps the same way);
 // QS16[t][q0][tau][c] = { bits(f32(-sum(I'))), bits(b_q) }.
 // Column groups: tile tau = w*GW + tw belongs to column group w (16*GW consecutive columns);
-// lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G: one group (k_level1_mf16);
-// GW = G/NW: one group per wave of k_level1_mfq.
+// lane c of that tile is window q1 = 16*GW*w + GW*c + tw.  GW = G/NW: one group per wave of
+// k_level1_mfq; GW = 16 B of output per lane for k_volume_ls.
 // WSC: window side known at compile time (0 = g.ws): the window's bytes are loaded once and
 // serve both the sums and the fragments.
 template <int WSC>
-__global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS, int bf)
+__global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 *QS)
 {
     DM_TAIL_ENTRY();
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -74,20 +72,6 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
     const int qx = __float_as_int((float)-s), qy = __float_as_int(bq); // exact: |s| <= 225*128
     QS[idx] = make_int2(qx, qy);
     const size_t tile = idx / 16; // (t, q0, tau)
-    if (bf) { // bf16 operands (v_mfma_f32_16x16x32_bf16, K = 32 >= n): lane c+16hq, taps 8hq..8hq+7
-        for (int hq = 0; hq < 4; ++hq) {
-            int w[4] = {0, 0, 0, 0};
-            for (int j = 0; j < 8; ++j) {
-                const int k = 8 * hq + j;
-                const int val = k < n ? px(k) : 0;
-                w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1))); // exact in bf16
-            }
-            dm_v4i o;
-            o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
-            Bw[tile * 64 + c + 16 * hq] = o;
-        }
-        return;
-    }
     // spread layout (KS == 1, n <= 32; build_a uses the same): lane c + 16 hq holds taps
     // 8 hq .. 8 hq + 7 in bytes 0..7 and the window's stats {qx, qy} in words 2, 3, which meet
     // A's zero bytes 8..15 -- every lane reads its own window's stats from its own fragment
@@ -171,13 +155,13 @@ __device__ __forceinline__ dm_v4i mfma16_tile(const dm_v4i *A, const dm_v4i *__r
 // packed instructions per voxel instead of 2.
 #define DM_YBIAS 0x4B400000
 
-template <bool YF, bool BF = false>
+template <bool YF>
 __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, const float *sTf, dm_f2 q2, int n,
                                          float *y)
 {
     if constexpr (YF) {
         const float nf = (float)n;
-        const float nb = BF ? 0.0f : -nf * 12582912.0f;   // exact (see above)
+        const float nb = -nf * 12582912.0f;   // exact (see above)
         const dm_f2 sI2 = __builtin_shufflevector(q2, q2, 0, 0), b2 = __builtin_shufflevector(q2, q2, 1, 1);
         const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
         const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
@@ -196,8 +180,8 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
 }
 
 // A operand of one lane: patch rows of a 2x2 cell block (row c: cell cl = c/4, child ch = c%4),
-// int8 taps 64ks + 16grp + j (i8 MFMA) or bf16 taps 8grp + j (BF, KS = 1)
-template <int KS, bool BF>
+// int8 taps 64ks + 16grp + j (spread layout, KS == 1 and n <= 32: taps 8grp + j)
+template <int KS>
 __device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, int J0, int c, int grp)
 {
     const int n = g.ws * g.ws;
@@ -207,13 +191,7 @@ __device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, 
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
         int w[4] = {0, 0, 0, 0};
-        if constexpr (BF) {
-            for (int j = 0; j < 8; ++j) {
-                const int k = 8 * grp + j;
-                const int val = k < n ? (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128 : 0;
-                w[j >> 1] |= (int)((__float_as_uint((float)val) >> 16) << (16 * (j & 1)));
-            }
-        } else if (KS == 1 && n <= 32) { // spread layout (k_prep_windows16): taps 8 grp + j
+        if (KS == 1 && n <= 32) { // spread layout (k_prep_windows16): taps 8 grp + j
             for (int j = 0; j < 8; ++j) {
                 const int k = 8 * grp + j;
                 int val = 0;
@@ -252,195 +230,23 @@ __device__ __forceinline__ float dpp_prev16_or(float v, float old)
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x111, 0xf, 0xf, false));
 }
 
-// one 16x16 tile: i8 MFMA onto acc0 (YF bias) or, BF, the bf16 MFMA whose f32 accumulator
-// is exact (integer partial sums < 2^24) -- returned as raw bits either way.
+// one 16x16 tile: i8 MFMA onto acc0 (YF bias), returned as raw bits.
 // K32 (spread layout: KS == 1, n <= 32): the taps sit in bytes 0..7 of every lane, 8 per
 // lane group -- exactly v_mfma_i32_16x16x32_i8's operand layout (k = 8 (lane >> 4) + j) -- so
 // the K = 32 instruction on the low 8 bytes gives the same exact sums as the K = 64 one (whose
 // bytes 8..15 are A's zeros against the window stats).  On gfx950 an MFMA keeps its SIMD
 // from issuing VALU while it runs (profiles/r03_valu_probe.txt), and the K = 32 form runs
 // half as long.
-template <int KS, bool BF, bool K32 = false>
+template <int KS, bool K32 = false>
 __device__ __forceinline__ dm_v4i mfma_tile(const dm_v4i *A, const dm_v4i *Bf, dm_v4i acc0)
 {
-    if constexpr (K32 && !BF) {
+    if constexpr (K32) {
         static_assert(KS == 1, "K = 32 form: one spread-layout fragment");
         const long a = (long)(((unsigned long)(unsigned)A[0].y << 32) | (unsigned)A[0].x);
         const long b = (long)(((unsigned long)(unsigned)Bf[0].y << 32) | (unsigned)Bf[0].x);
         return __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, acc0, 0, 0, 0);
-    } else if constexpr (BF) {
-        typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        v4f c = {0.0f, 0.0f, 0.0f, 0.0f};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, A[0]), __builtin_bit_cast(v8bf, Bf[0]),
-                                                     c, 0, 0, 0);
-        return __builtin_bit_cast(dm_v4i, c);
     } else {
         return mfma16_frag_c<KS>(A, Bf, acc0);
-    }
-}
-
-__device__ __forceinline__ float shfl_prev16(float v, int lane)
-{
-    const float o = __shfl(v, lane - 1);
-    return (lane & 15) == 0 ? -INFINITY : o; // no q1 = -1 left of column 0
-}
-
-template <int KS, int G, int MINW, bool PF>
-__global__ __launch_bounds__(256, MINW) void k_level1_mf16(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                     const int2 *__restrict__ QS, double *L1)
-{
-    __shared__ PowLds plds;
-    const int tid = threadIdx.x;
-    pow_lds_fill(plds, tid, 256);
-    __syncthreads();
-
-    const int lane = tid & 63, wave = tid >> 6;
-    const int c = lane & 15, grp = lane >> 4;
-    const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
-    const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
-    const int nbj = w1 / 2, bpt = ((h0 / 2) / 2) * nbj; // 2x2-cell blocks per tile
-    const int gb = blockIdx.x * MF_WAVES + wave;
-    const int t = gb / bpt;
-    if (t >= g.T) return; // whole wave exits (no block-level sync below)
-    const int I0 = 2 * ((gb % bpt) / nbj), J0 = 2 * ((gb % bpt) % nbj);
-    const size_t tb = (size_t)t * P;
-    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-
-    // A operand: patch row rho = c: cell rho>>2, child rho&3 (build_a: the tap layout of
-    // k_prep_windows16's fragments)
-    dm_v4i A[KS];
-    build_a<KS, false>(A, g, t, I0, J0, c, grp);
-    // this lane's cell (grp) and its 4 children (acc[reg], reg = child)
-    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
-    int sTr[4], pidx[4];
-    float ar[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        pidx[r] = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
-        sTr[r] = s.sT[tb + pidx[r]];
-        ar[r] = s.aP[tb + pidx[r]];
-    }
-    const dm_v4i *Bt = Bw + (size_t)t * h0 * G * KS * 64;
-    const int2 *Qt = QS + (size_t)t * h0 * G * 16;
-
-    // ---- sweep 1: per-patch min / max of y (next tile's B / window stats prefetched) ----
-    float mn[4], mx[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
-    const int NT = h0 * G;
-    dm_v4i bn[KS];
-    int2 qn;
-    if constexpr (PF) {
-        load_frag<KS>(bn, Bt, lane);
-        qn = Qt[c];
-    }
-    for (int ti = 0; ti < NT; ++ti) {
-        dm_v4i bc[KS];
-        int2 qs;
-        if constexpr (PF) { // software prefetch of the next tile
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) bc[ks] = bn[ks];
-            qs = qn;
-            const int tn = ti + 1 < NT ? ti + 1 : ti;
-            load_frag<KS>(bn, Bt + (size_t)tn * KS * 64, lane);
-            qn = Qt[tn * 16 + c];
-        } else {
-            load_frag<KS>(bc, Bt + (size_t)ti * KS * 64, lane);
-            qs = Qt[ti * 16 + c];
-        }
-        const dm_v4i acc = mfma16_frag<KS>(A, bc);
-        const float b = __int_as_float(qs.y);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float y = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
-            mn[r] = fminf(mn[r], y);
-            mx[r] = fmaxf(mx[r], y);
-        }
-    }
-    float rmn[4], den[4], rinv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        for (int off = 1; off < 16; off <<= 1) {
-            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
-            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
-        }
-        rmn[r] = r_of_y(mn[r], ar[r], g.method);
-        const float rmx = r_of_y(mx[r], ar[r], g.method);
-        den[r] = __fsub_rn(rmx, rmn[r]);
-        rinv[r] = __frcp_rn(den[r]);
-        if (c == 0) { s.rmn[tb + pidx[r]] = rmn[r]; s.rmx[tb + pidx[r]] = rmx; }
-    }
-
-    // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 ----
-    // tile order per row: tau = G-1 first (its value feeds lane c+1), then 0 .. G-2
-    constexpr int M = G / 2; // pooled columns per lane: v = M*c + m
-    float Racc[M][4], Cprev[M][4];
-    double *Lrow = L1 + ((size_t)t * P1 + (size_t)Ic * w1 + Jc) * P1;
-    if constexpr (PF) {
-        load_frag<KS>(bn, Bt + (size_t)(G - 1) * KS * 64, lane);
-        qn = Qt[(G - 1) * 16 + c];
-    }
-    for (int q0 = 0; q0 < h0; ++q0) {
-        float Cm[M][4], prev[4], xlast[4];
-        const int q0n = q0 + 1 < h0 ? q0 + 1 : q0;
-#pragma unroll
-        for (int it = 0; it < G; ++it) {
-            const int tau = it == 0 ? G - 1 : it - 1;
-            dm_v4i bc[KS];
-            int2 qs;
-            if constexpr (PF) {
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) bc[ks] = bn[ks];
-                qs = qn;
-                const int tn = it + 1 < G ? q0 * G + it : q0n * G + G - 1; // (row, tau) of the next tile
-                load_frag<KS>(bn, Bt + (size_t)tn * KS * 64, lane);
-                qn = Qt[tn * 16 + c];
-            } else {
-                load_frag<KS>(bc, Bt + (size_t)(q0 * G + tau) * KS * 64, lane);
-                qs = Qt[(q0 * G + tau) * 16 + c];
-            }
-            const dm_v4i acc = mfma16_frag<KS>(A, bc);
-            const float b = __int_as_float(qs.y);
-            float y[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = __fmul_rn((float)(__mul24(acc[r], n) + __mul24(sTr[r], (int)__int_as_float(qs.x))), b);
-            if (it == 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { xlast[r] = y[r]; prev[r] = shfl_prev16(y[r], lane); }
-            } else if ((tau & 1) == 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Cm[tau / 2][r] = fmaxf(prev[r], y[r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { Cm[tau / 2][r] = fmaxf(Cm[tau / 2][r], y[r]); prev[r] = y[r]; }
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Cm[M - 1][r] = fmaxf(Cm[M - 1][r], xlast[r]);
-        if ((q0 & 1) == 0) {
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Racc[m][r] = q0 == 0 ? Cm[m][r] : fmaxf(Cprev[m][r], Cm[m][r]);
-            continue;
-        }
-        const int u = q0 >> 1;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            // (measured: computing the 4 fast pows branch-free and patching 0 / NaN afterwards
-            // needs more registers and ran 12-30 % slower than this per-child form)
-            double sum = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
-                const float R = fmaxf(Racc[m][r], Cm[m][r]);
-                Cprev[m][r] = Cm[m][r];
-                const float x = norm_mk(r_of_y_fast(R, ar[r], g.method), rmn[r], den[r], rinv[r]);
-                const double pv = pow14_lds((double)x, plds);
-                sum = r == 0 ? pv : sum + pv;
-            }
-            Lrow[(size_t)u * w1 + M * c + m] = pow14_lds(sum / 4.0, plds);
-        }
     }
 }
 
@@ -523,11 +329,11 @@ struct XchOwn<true, T, OFF> {
 // NB 2x2-cell blocks per workgroup (NB = 2 where one wave spans a whole tile row, S = 64):
 // waves sb * NWc .. sb * NWc + NWc - 1 split block sb's columns; the blocks share the pow
 // tables, which is what a workgroup of more than one wave buys there.
-template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, bool BF = false, int NB = 1, bool CL = false>
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, int NB = 1, bool CL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                         const int2 *__restrict__ QS, double *L1, double *L2)
 {
-    constexpr bool EQ = KS == 1 && YF && !BF;    // window stats ride in the B tile (qs_of_frag)
+    constexpr bool EQ = KS == 1 && YF;           // window stats ride in the B tile (qs_of_frag)
     static_assert(NW % NB == 0, "blocks split the waves evenly");
     static_assert(!CL || L2F, "clamp-bit normalisation: NaN cells are restored at the level-2 / level-1 stores");
     constexpr int NWc = NW / NB;                 // waves per cell block
@@ -587,7 +393,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
+    build_a<KS>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
     float sTf[4];
@@ -636,9 +442,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto minmax_row = [&](const RowFrag &f) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma_tile<KS, BF, EQ>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, EQ>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
+            y_of_acc<YF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 mn[r] = fminf(mn[r], y[r]);
@@ -708,9 +514,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     auto pool_cols = [&](const RowFrag &f, float (&Cm)[M][4], float (&last)[4]) {
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
-            const dm_v4i acc = mfma_tile<KS, BF, EQ>(A, f.b[tw], acc0);
+            const dm_v4i acc = mfma_tile<KS, EQ>(A, f.b[tw], acc0);
             float y[4];
-            y_of_acc<YF, BF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
+            y_of_acc<YF>(acc, sTr, sTf, EQ ? qs_of_frag(f.b[tw][0]) : qs_pair(f.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if ((tw & 1) == 0) Cm[tw / 2][r] = tw == 0 ? y[r] : fmaxf(last[r], y[r]);
@@ -907,9 +713,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 // lane c's GW tiles of group g are GW consecutive floats: one GW-float vector store per
 // patch, a 16-lane group writing 64*GW/... = 16*GW*4 contiguous bytes of the patch's row.
 // ===================================================================================
-template <int KS, int GW, bool YF, bool NT, bool LS, bool BF = false>
+// OT = float (co_map) or _Float16 (the binary16 volume: the float32 value rounded to nearest
+// even, as np.float16(co_map)).  Used for the shapes k_volume_ls does not take (ws > 5).
+template <int KS, int GW, bool YF, bool NT, bool LS, typename OT = float>
 __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                    const int2 *__restrict__ QS, float *vol)
+                                                    const int2 *__restrict__ QS, OT *vol)
 {
     // LS: a row's 16 x w0 results are staged in LDS and stored as whole patch rows
     // (w0 * 4 contiguous bytes per patch, 16-B lanes) instead of GW-float pieces
@@ -927,7 +735,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
+    build_a<KS>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4], pr[4];
     float sTf[4], ap[4];
@@ -974,7 +782,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, qs_pair(fa.q[tw]), n, y);
+            y_of_acc<YF>(mfma_tile<KS>(A, fa.b[tw], acc0), sTr, sTf, qs_pair(fa.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -982,7 +790,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, qs_pair(fb.q[tw]), n, y);
+            y_of_acc<YF>(mfma_tile<KS>(A, fb.b[tw], acc0), sTr, sTf, qs_pair(fb.q[tw]), n, y);
 #pragma unroll
             for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
         }
@@ -1008,6 +816,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
     }
 
     typedef float fv __attribute__((ext_vector_type(GW)));
+    typedef OT ofv __attribute__((ext_vector_type(GW)));
     float *stg = &stage[LS ? wv : 0][0];
     const size_t pbase = tb + (size_t)(2 * I0) * w0 + 2 * J0; // patch (row 2*I0, col 2*J0)
     auto emit = [&](const Unit &f, int uidx) {
@@ -1016,7 +825,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 #pragma unroll
         for (int tw = 0; tw < GW; ++tw) {
             float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, qs_pair(f.q[tw]), n, y);
+            y_of_acc<YF>(mfma_tile<KS>(A, f.b[tw], acc0), sTr, sTf, qs_pair(f.q[tw]), n, y);
             // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
             const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
             const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
@@ -1041,9 +850,12 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
             if constexpr (LS) {
                 *(fv *)(stg + (4 * grp + r) * w0 + col) = v;
             } else {
-                fv *dst = (fv *)(vol + (tb + pr[r]) * (size_t)P + (size_t)q0 * w0 + col);
-                if constexpr (NT) __builtin_nontemporal_store(v, dst);
-                else *dst = v;
+                ofv ov;
+#pragma unroll
+                for (int tw = 0; tw < GW; ++tw) ov[tw] = (OT)v[tw];
+                ofv *dst = (ofv *)(vol + (tb + pr[r]) * (size_t)P + (size_t)q0 * w0 + col);
+                if constexpr (NT) __builtin_nontemporal_store(ov, dst);
+                else *dst = ov;
             }
         }
         if constexpr (LS) {
@@ -1056,12 +868,14 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
                 for (int j = 0; j < 16; j += rows_per) {
                     const int pl = j + lane / per, k4 = lane % per; // local patch 4*cell + child
                     typedef float f4v __attribute__((ext_vector_type(4)));
+                    typedef OT o4v __attribute__((ext_vector_type(4)));
                     const f4v v4 = *(const f4v *)(stg + pl * w0 + 4 * k4);
+                    const o4v o4 = {(OT)v4.x, (OT)v4.y, (OT)v4.z, (OT)v4.w};
                     const int pc = pl >> 2, pch = pl & 3;
                     const size_t prow = pbase + (size_t)(2 * (pc >> 1) + (pch >> 1)) * w0 + 2 * (pc & 1) + (pch & 1);
-                    f4v *dst = (f4v *)(vol + prow * (size_t)P + (size_t)q0 * w0) + k4;
-                    if constexpr (NT) __builtin_nontemporal_store(v4, dst);
-                    else *dst = v4;
+                    o4v *dst = (o4v *)(vol + prow * (size_t)P + (size_t)q0 * w0) + k4;
+                    if constexpr (NT) __builtin_nontemporal_store(o4, dst);
+                    else *dst = o4;
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -1072,179 +886,6 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
         emit(fa, ui);
         load_unit(fa, ui + 2 < NU ? ui + 2 : 0);
         emit(fb, ui + 1);
-    }
-}
-
-// ===================================================================================
-// Level-0 volume, column-split (the k_level1_mfq workgroup shape): NW waves share 16
-// patches, wave w sweeps column group w.  Per-patch min/max are reduced through LDS once;
-// in sweep 2 the waves fill a shared LDS stage of RB rows x w0 windows x 16 patches and the
-// workgroup stores it as 16 contiguous runs of RB*w0*4 bytes (one per patch) with 16-B
-// non-temporal stores -- longer HBM write runs than one wave can stage alone.
-// ===================================================================================
-// OT = float (co_map, 4 B/voxel) or _Float16 (the fp16 volume of BASELINE config C5,
-// 2 B/voxel: the float32 value rounded to nearest-even binary16, as np.float16(co_map)).
-template <int KS, int GW, int NW, int RB, bool YF, int MINW = 1, bool BF = false, typename OT = float>
-__global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                       const int2 *__restrict__ QS, OT *vol)
-{
-    constexpr int G = GW * NW, W0 = 16 * G; // w0 is a template constant here
-    constexpr int EV = 16 / sizeof(OT);     // elements per 16-B store
-    __shared__ __attribute__((aligned(16))) OT stage[16][RB][W0];
-    __shared__ float red[2][NW][16];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int c = lane & 15, grp = lane >> 4;
-    const int h0 = g.h0, n = g.ws * g.ws, P = h0 * W0;
-    const int nbj = W0 / 4, bpt = (h0 / 4) * nbj;
-    const int t = blockIdx.x / bpt;
-    const int I0 = 2 * ((blockIdx.x % bpt) / nbj), J0 = 2 * ((blockIdx.x % bpt) % nbj);
-    const size_t tb = (size_t)t * P;
-    const int ro = g.org[2 * t], co = g.org[2 * t + 1];
-
-    dm_v4i A[KS];
-    build_a<KS, BF>(A, g, t, I0, J0, c, grp);
-    const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
-    int sTr[4];
-    float sTf[4], ap[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
-        sTr[r] = s.sT[tb + p];
-        sTf[r] = (float)sTr[r];
-        ap[r] = s.aP[tb + p];
-    }
-    const int ab = YF ? DM_YBIAS : 0;
-    const dm_v4i acc0 = {ab, ab, ab, ab};
-    const unsigned mant = mant_mask_vgpr();   // pow14_zf's mantissa mask, kept in a VGPR
-    const dm_v4i *Bt = Bw + ((size_t)t * h0 * G + wave * GW) * KS * 64;
-    const int2 *Qt = QS + ((size_t)t * h0 * G + wave * GW) * 16;
-    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void *)Bt, 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc((void *)Qt, 0, 0x7fffffff, 0x00020000);
-    const unsigned voB = (unsigned)lane * 16u, voQ = (unsigned)c * 8u;
-    struct RowFrag {
-        dm_v4i b[GW][KS];
-        int2 q[GW];
-    };
-    auto load_row = [&](RowFrag &f, int q0) {
-#pragma unroll
-        for (int tw = 0; tw < GW; ++tw) {
-            const unsigned ti = (unsigned)q0 * G + tw;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                f.b[tw][ks] = __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (ti * KS + ks) * 1024u, 0);
-            const dm_v2i qv = __builtin_amdgcn_raw_buffer_load_b64(rQ, voQ, ti * 128u, 0);
-            f.q[tw] = make_int2(qv.x, qv.y);
-        }
-    };
-
-    // ---- sweep 1: min / max of y over this wave's columns, then over the waves ----
-    float mn[4], mx[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { mn[r] = INFINITY; mx[r] = -INFINITY; }
-    RowFrag fa, fb;
-    load_row(fa, 0);
-    for (int q0 = 0; q0 < h0; q0 += 2) {
-        load_row(fb, q0 + 1);
-#pragma unroll
-        for (int tw = 0; tw < GW; ++tw) {
-            float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fa.b[tw], acc0), sTr, sTf, qs_pair(fa.q[tw]), n, y);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
-        }
-        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
-#pragma unroll
-        for (int tw = 0; tw < GW; ++tw) {
-            float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, fb.b[tw], acc0), sTr, sTf, qs_pair(fb.q[tw]), n, y);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { mn[r] = fminf(mn[r], y[r]); mx[r] = fmaxf(mx[r], y[r]); }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        for (int off = 1; off < 16; off <<= 1) {
-            mn[r] = fminf(mn[r], __shfl_xor(mn[r], off));
-            mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
-        }
-        if (c == 0) { red[0][wave][4 * grp + r] = mn[r]; red[1][wave][4 * grp + r] = mx[r]; }
-    }
-    __syncthreads();
-    float lo[4], hi[4], rmn[4], den[4], rinv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        float a = red[0][0][4 * grp + r], b = red[1][0][4 * grp + r];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) { a = fminf(a, red[0][w][4 * grp + r]); b = fmaxf(b, red[1][w][4 * grp + r]); }
-        rmn[r] = r_of_y(a, ap[r], g.method);
-        const float rmx = r_of_y(b, ap[r], g.method);
-        den[r] = __fsub_rn(rmx, rmn[r]);
-        rinv[r] = __frcp_rn(den[r]);
-        const bool cc = g.method == DM_TM_CCOEFF;
-        lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
-        hi[r] = cc ? INFINITY : 1.0f;
-        if (wave == 0 && c == 0) {
-            const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
-            s.rmn[tb + p] = rmn[r];
-            s.rmx[tb + p] = rmx;
-        }
-    }
-
-    // ---- sweep 2: x for this wave's columns -> stage; every RB rows the workgroup stores ----
-    typedef OT fv __attribute__((ext_vector_type(GW)));
-    typedef OT f4v __attribute__((ext_vector_type(EV)));
-    auto emit = [&](const RowFrag &f, int q0) {
-        float xs[GW][4];
-#pragma unroll
-        for (int tw = 0; tw < GW; ++tw) {
-            float y[4];
-            y_of_acc<YF, BF>(mfma_tile<KS, BF>(A, f.b[tw], acc0), sTr, sTf, qs_pair(f.q[tw]), n, y);
-            // r = med3(y * a_p, lo, hi); x = (r - rmin) / den (norm_mk's Markstein), packed
-            const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
-            const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
-            const float rr[4] = {__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1]),
-                                 __builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
-            const dm_f2 a01 = dm_f2{rr[0], rr[1]} - dm_f2{rmn[0], rmn[1]};
-            const dm_f2 a23 = dm_f2{rr[2], rr[3]} - dm_f2{rmn[2], rmn[3]};
-            const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
-            const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
-            const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
-            const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
-            const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
-            const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
-            xs[tw][0] = x01.x; xs[tw][1] = x01.y; xs[tw][2] = x23.x; xs[tw][3] = x23.y;
-        }
-        const int col = 16 * GW * wave + GW * c, slot = q0 % RB;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            fv v;
-#pragma unroll
-            for (int tw = 0; tw < GW; ++tw) v[tw] = (OT)xs[tw][r];
-            *(fv *)&stage[4 * grp + r][slot][col] = v;
-        }
-        if (slot == RB - 1) {
-            __syncthreads();
-            constexpr int PER = RB * W0 / EV;  // 16-B vectors per patch run
-            constexpr int TOT = 16 * PER;
-            const size_t pbase = tb + (size_t)(2 * I0) * W0 + 2 * J0;
-            const int qbase = (q0 - RB + 1) * W0;
-#pragma unroll
-            for (int i = tid; i < TOT; i += 64 * NW) {
-                const int pl = i / PER, k4 = i % PER;
-                const f4v v4 = *(const f4v *)(&stage[pl][0][0] + EV * k4);
-                const int pc = pl >> 2, pch = pl & 3;
-                const size_t prow = pbase + (size_t)(2 * (pc >> 1) + (pch >> 1)) * W0 + 2 * (pc & 1) + (pch & 1);
-                __builtin_nontemporal_store(v4, (f4v *)(vol + prow * (size_t)P + qbase) + k4);
-            }
-            __syncthreads();
-        }
-    };
-    for (int q0 = 0; q0 < h0; q0 += 2) {
-        load_row(fb, q0 + 1);
-        emit(fa, q0);
-        load_row(fa, q0 + 2 < h0 ? q0 + 2 : 0);
-        emit(fb, q0 + 1);
     }
 }
 
@@ -1264,7 +905,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_volume_cs(Geo g, Stats s, con
 // after a group a lane holds GW consecutive windows of each of its 4 patches and writes them
 // with one 16-B store straight from registers: 16 lanes = one contiguous 256-B patch-row
 // run per store instruction, no LDS stage.
-// Arithmetic per voxel is k_volume_cs's (same y, r, Markstein x): bit-identical output.
+// Arithmetic per voxel is k_volume_mfq's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
 template <int G, int NW, bool NT, typename OT, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
@@ -1290,7 +931,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
     const size_t tb = (size_t)t * P;
 
     dm_v4i A[1];
-    build_a<1, false>(A, g, t, I0, J0, c, grp);
+    build_a<1>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
     float sTf[4], ap[4];
@@ -1327,7 +968,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         const dm_v4i bf = *(const dm_v4i *)&lds[buf * BUF + tau * 1024 + lane * 16];
         const dm_f2 q2 = qs_of_frag(bf); // {qx, qy}
         dm_v4i bfr[1] = {bf};
-        y_of_acc<true, false>(mfma_tile<1, false, true>(A, bfr, acc0), sTr, sTf, q2, n, y);
+        y_of_acc<true>(mfma_tile<1, true>(A, bfr, acc0), sTr, sTf, q2, n, y);
     };
 
     float lo[4], hi[4], rmn[4], den[4], rinv[4];

@@ -299,6 +299,8 @@ __global__ __launch_bounds__(64) void k_seq_sum(const double *__restrict__ v, lo
 // as the reference's one float64 add, where the binade changes: s + inc u reaches 2^(e+1), or
 // d is not finite or not below 2^(e+1) -- once per binade the sum climbs (a few dozen over a
 // sweep).  NaN / inf in s: the rest is added one by one (NaN + x, inf + x as the chain does).
+// A negative term (dm_seq_sum is a public entry; the reference's callers only pass abs())
+// is also a step of its own, and once s is negative the rest is added one by one.
 // Bit-identical to k_seq_sum (tests/test_seq_sum_gpu.py).
 constexpr int SEG_T = 1024, SEG_E = 8, SEG_CH = SEG_T * SEG_E;
 
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(SEG_T) void k_seq_sum_seg(const double *__restrict_
     double s = 0.0;
     long long k0 = 0;
     for (int it = 0; k0 < n; it ^= 1) {
-        if (!(s < INFINITY)) { // NaN or inf (uniform)
+        if (!(s >= 0.0 && s < INFINITY)) { // NaN, inf or a negative sum (uniform): the chain
             if (t == 0) {
                 for (long long k = k0; k < n; ++k) s += v[k];
                 *out = s;
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(SEG_T) void k_seq_sum_seg(const double *__restrict_
             const double d = kt + i < n ? v[kt + i] : 0.0;
             const double f = ldexp(d, sh);    // exact (d < B: f < 2^53)
             const double fl = floor(f);
-            const bool bad = !(d < B);
+            const bool bad = !(d >= 0.0 && d < B);   // negative terms: a step of their own
             const bool ti = !bad && f - fl == 0.5;
             q[i] = bad ? 0ull : (u64)(ti ? fl : rint(f));
             if (bad && lbad == SEG_E) lbad = i;

@@ -148,6 +148,12 @@ class DevicePyramid:
     def compute_stats(self):
         if not self._have_stats:
             ss = self._stats_stream
+            if ss is not None:
+                # forward order: the images / origins may have been written on this pyramid's
+                # own stream (a conversion, a non-blocking upload); the stats read them
+                ready = torch.cuda.Event()
+                ready.record(self.stream if self.stream is not None else torch.cuda.current_stream())
+                ss.wait_event(ready)
             L.check(self.lib.dm_corr_stats(self.b.ref(), L.ptr(self.stats),
                                            L.stream_handle(ss) if ss is not None else self._s()),
                     'dm_corr_stats')

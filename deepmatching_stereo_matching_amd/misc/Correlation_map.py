@@ -67,11 +67,11 @@ class LevelList(Sequence):
 
     def __delitem__(self, k):
         if isinstance(k, slice):
-            start, stop, step = k.indices(len(self))
-            if step == 1 and stop >= len(self) and start < len(self):
-                self._n = start
+            idx = sorted(range(*k.indices(len(self))))
+            if not idx:                      # an empty cut deletes nothing, as on a list
                 return
-            if start >= stop:
+            if idx == list(range(idx[0], len(self))):   # a top suffix, in either direction
+                self._n = idx[0]
                 return
         elif self._index(k) == len(self) - 1:
             self._n -= 1

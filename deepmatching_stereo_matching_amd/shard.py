@@ -52,6 +52,12 @@ def tile_sharding_enabled():
     return bool(on) and world()[1] > 1
 
 
+def _group():
+    """True when a process group is initialised: the gathers then always run the collective,
+    at world size 1 too (a one-rank RCCL group is still exercised end to end)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def rank_units(n, rank, size):
     """Units of this rank: round robin (balanced to within one unit)."""
     return list(range(rank, n, size))
@@ -63,12 +69,13 @@ def _gather_units(local, n, rank, size, shape, dtype):
     (CPU tests, or ranks sharing one GPU) gathers host copies and the result goes back to
     ``local``'s device."""
     per = (n + size - 1) // size
-    host = size > 1 and local.is_cuda and dist.get_backend() == 'gloo'
+    group = _group()
+    host = group and local.is_cuda and dist.get_backend() == 'gloo'
     dev = local.device
     buf = torch.zeros((per,) + tuple(shape), dtype=dtype, device='cpu' if host else dev)
     if len(local):
         buf[:len(local)] = local
-    if size == 1:
+    if not group:
         return buf[:n]
     parts = [torch.empty_like(buf) for _ in range(size)]
     dist.all_gather(parts, buf)
@@ -88,7 +95,8 @@ def gather_units_to(local, n, rank, size, dst=0):
     copies; the result goes back to ``local``'s device."""
     shape, dtype = tuple(local.shape[1:]), local.dtype
     per = (n + size - 1) // size
-    host = size > 1 and local.is_cuda and dist.get_backend() == 'gloo'
+    group = _group()
+    host = group and local.is_cuda and dist.get_backend() == 'gloo'
     dev = local.device
     if len(local) == per and not host:
         buf = local.contiguous()
@@ -96,7 +104,7 @@ def gather_units_to(local, n, rank, size, dst=0):
         buf = torch.zeros((per,) + shape, dtype=dtype, device='cpu' if host else dev)
         if len(local):
             buf[:len(local)] = local
-    if size == 1:
+    if not group:
         return buf[:n]
     parts = [torch.empty_like(buf) for _ in range(size)] if rank == dst else None
     dist.gather(buf, parts, dst=dst)

@@ -1,0 +1,76 @@
+"""bench.py's host logic on CPU: the roofline fraction is tied to the build it describes
+(VERDICT r3 "Next" 5).  The committed profiles carry the sha256 of the profiled kernel's
+machine code + descriptor (tools/kernel_hash.py, read from the gfx950 code objects inside
+libdmstereo.so); bench.py reports frac: null with the reason when the loaded library's kernel
+differs."""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'tools'))
+
+
+@pytest.fixture(scope='module')
+def bench():
+    import bench as b
+    return b
+
+
+def test_every_profiled_kernel_is_in_the_library():
+    import kernel_hash as K
+    hashes = {}
+    for tile in K.LEVEL:
+        hashes[('level', tile)] = K.kernel_hash(K.symbol('level', tile))
+    for tile, esz in K.VOLUME:
+        hashes[('volume', tile, esz)] = K.kernel_hash(K.symbol('volume', tile, esz))
+    assert all(h and len(h) == 16 for h in hashes.values()), hashes
+    assert len(set(hashes.values())) == len(hashes)          # distinct instances
+    assert K.kernel_hash('no_such_kernel') is None
+    assert K.kernel_hash('k_level1_mfq') is None             # ambiguous: many instances
+
+
+class _Batch:
+    T = 64
+
+
+class _Solver:
+    batch = _Batch()
+
+
+def test_frac_null_for_a_stale_profile(bench, monkeypatch):
+    import kernel_hash as K
+    cur = K.kernel_hash(K.symbol('level', 128))
+    good = {'tile': 128, 'tiles': 64, 'issue_cycles_per_launch': 13.0e9, 'gpu_cycles_per_launch': 14.0e6,
+            'clock_ghz': 1.7, 'kernel_ms_profiled': 8.0, 'hbm_bytes_per_launch': 1.2e9,
+            'issue_model_isa_sha16': cur, 'isa_sha16': cur}
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: dict(good))
+    r = bench.level_roofline(_Solver(), 128, 7.5)
+    assert r['frac'] == pytest.approx(13.0e9 / 7.5e-3 / 1e9 / (1024 * 2.4), abs=1e-4)
+    assert r['traffic'] == 1.2e9 and 'issue_occupancy_profiled' in r
+
+    stale = dict(good, issue_model_isa_sha16='0123456789abcdef')
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: dict(stale))
+    r = bench.level_roofline(_Solver(), 128, 7.5)
+    assert r['frac'] is None and r['achieved'] is None
+    assert 'stale profile' in r['source']['issue_cycles_per_launch']
+    assert r['traffic'] == 1.2e9                            # the PMC pass itself is current
+
+    stale_pmc = dict(good, isa_sha16=None)
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: dict(stale_pmc))
+    r = bench.level_roofline(_Solver(), 128, 7.5)
+    assert r['frac'] is not None                            # model current
+    assert r['traffic'] is None and 'issue_occupancy_profiled' not in r
+    assert 'stale profile' in r['isa_check']['pmc']
+
+
+def test_volume_traffic_needs_a_current_profile(bench, monkeypatch):
+    import kernel_hash as K
+    cur = K.kernel_hash(K.symbol('volume', 128, 2))
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {'hbm_bytes_per_launch': 35e9, 'isa_sha16': cur})
+    assert bench.load_traffic(128, 'volume_f16', 64) == 35e9
+    assert bench.load_traffic(128, 'volume', 64) is None     # float32 instance: other bytes
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {'hbm_bytes_per_launch': 35e9})
+    assert bench.load_traffic(128, 'volume_f16', 64) is None

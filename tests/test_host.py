@@ -205,3 +205,13 @@ def test_level_list_cuts_like_a_list():
         ll.pop(0)
     del ll[4]
     assert len(ll) == 4
+    # negative steps: an empty cut deletes nothing; a top suffix taken backwards drops it;
+    # any other cut (a plain list would delete those items) raises
+    del ll[2:2:-1]
+    assert len(ll) == 4
+    del ll[:1:-1]                      # items 3, 2: the top suffix from level 2
+    assert len(ll) == 2
+    with pytest.raises(TypeError):
+        del ll[-2::-1]                 # item 0 only: not a top suffix
+    del ll[::-2]                       # item 1: the top
+    assert len(ll) == 1

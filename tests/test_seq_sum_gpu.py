@@ -84,6 +84,11 @@ def _cases():
         'nan_middle': np.concatenate([rng.random(10000), [np.nan], rng.random(10000)]),
         'inf_then_nan': np.concatenate([rng.random(9000), [np.inf], rng.random(10), [np.nan], rng.random(10)]),
         'inf_only': np.concatenate([rng.random(100), [np.inf], rng.random(9000)]),
+        # dm_seq_sum is a public entry point: negative terms (the reference's callers pass abs()
+        # values only) are steps of their own, and a negative running sum adds one by one
+        'negative_terms': np.where(rng.random(30000) < 0.01, -1.0, 1.0) * np.abs(rng.standard_normal(30000)),
+        'negative_sum': np.concatenate([rng.random(5000), [-1e6], rng.random(20000), [2e6], rng.random(9000)]),
+        'negative_zero': np.concatenate([[-0.0], rng.random(100), [-0.0, -1e-300]]),
     }
 
 
@@ -98,7 +103,7 @@ def test_seq_sum_bit_exact(lib, name):
     assert _same(got, want), (name, got, want)
 
 
-@pytest.mark.parametrize('name', ['sweep_errors', 'ties', 'log_uniform_range', 'nan_middle'])
+@pytest.mark.parametrize('name', ['sweep_errors', 'ties', 'log_uniform_range', 'nan_middle', 'negative_sum'])
 def test_seq_sum_equals_chain_kernel(lib, name):
     v = CASES[name]
     assert _same(_dev(lib, v), _dev(lib, v, 'chain'))

@@ -21,13 +21,14 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'tools'))
 import isa_cost  # noqa: E402
+import kernel_hash  # noqa: E402
 
 KERNELS = {  # shape -> (kernel symbol substring, weights file, pmc file, waves per launch)
-    'c3': ('k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELb0ELi1ELb1EE', 'issue_model_level1_c3_weights.json',
+    'c3': ('k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi1ELb1EE', 'issue_model_level1_c3_weights.json',
            'pmc_level1.json', 64 * (128 // 4) * (128 // 4) * 2),
-    'c2': ('k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELb0ELi2ELb1EE', 'issue_model_level1_c2_weights.json',
+    'c2': ('k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi2ELb1EE', 'issue_model_level1_c2_weights.json',
            'pmc_level1_s64.json', 64 * (64 // 4) * (64 // 4)),
-    'c5': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELb0ELi1ELb1EE', 'issue_model_level1_c5_weights.json',
+    'c5': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE', 'issue_model_level1_c5_weights.json',
            'pmc_level1_s256.json', 256 * (256 // 4) * (256 // 4) * 4),
 }
 
@@ -65,6 +66,9 @@ def main():
         d['issue_model_cycles_per_wave'] = round(cyc, 1)
         d['waves_per_launch'] = waves
         d['issue_cycles_per_launch'] = cyc * waves
+        # the in-tree library built from the same source the asm was compiled from: bench.py
+        # prices a launch with this model only while it loads the same kernel bytes
+        d['issue_model_isa_sha16'] = kernel_hash.kernel_hash(kern)
         pmc = d.get('valu_insts_per_launch')
         check = ''
         if pmc:

@@ -1,7 +1,9 @@
-"""Kernel A/B timer: dm_corr_level1 variants on the C3 workload, interleaved rounds in one
-process (cdna_hip_programming.md section 5.4 rule 24).
+"""Level-kernel timer on the C3 workload: dm_corr_level12 ('l12', level 2 fused) and/or
+dm_corr_level1 ('l1'), interleaved rounds in one process (cdna_hip_programming.md section 5.4
+rule 24).  Library builds are A/B'd with DM_LIB_PATH (tools/ab3.sh): the kernel variants are
+a function of the shape, not of the environment.
 
-    python tools/kbench.py [--variants mf16,mf32,generic] [--rounds 5] [--tile 128] [--tiles 64]
+    python tools/kbench.py [--variants l12,l1] [--rounds 5] [--tile 128] [--grid 8]
 """
 import argparse
 import os
@@ -18,7 +20,7 @@ from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--variants', default='mf16,mf32')
+    ap.add_argument('--variants', default='l12')
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--tile', type=int, default=128)
     ap.add_argument('--grid', type=int, default=8)
@@ -36,15 +38,7 @@ def main():
     outs = {}
     for rnd in range(args.rounds + 1):
         for v in res:
-            # "mf16+DM_MF16_MINW=4": kernel variant plus extra environment settings
-            parts = v.split('+')
-            fused = parts[0] == 'l12'       # dm_corr_level12 (level 2 fused, level 1 on chip)
-            os.environ['DM_LEVEL1'] = 'mfq' if fused else parts[0]
-            for kv in ('DM_MF16_MINW', 'DM_MF16_PF', 'DM_MFQ_MINW', 'DM_MFQ_NWMAX', 'DM_MFQ_GW', 'DM_MFQ_CLAMP'):
-                os.environ.pop(kv, None)
-            for kv in parts[1:]:
-                k, val = kv.split('=')
-                os.environ[k] = val
+            fused = v == 'l12'       # dm_corr_level12 (level 2 fused, level 1 on chip); else level 1
             batch = engine.TileBatch(ia, ib, org, S, S, ws, L.DM_TM_CCOEFF_NORMED, dev)
             pyr = engine.DevicePyramid(batch, build=False).compute_stats()
             P2 = P1 // 4

@@ -19,6 +19,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import kernel_hash  # noqa: E402
+
 SHAPES = {  # shape -> (kernel prefix, f16 instantiation?, json name, tile, tiles)
     'l12_c3': ('k_level1_mfq', None, 'pmc_level1.json', 128, 64),
     'l12_c5': ('k_level1_mfq', None, 'pmc_level1_s256.json', 256, 256),
@@ -90,6 +93,12 @@ def main(root):
             continue
         d = {'kernel': prefix + (' (binary16)' if f16 else ''), 'tile': tile, 'tiles': tiles,
              'source': 'tools/pmc_r03.sh %s (rocprofv3 --kernel-trace --pmc, separate passes)' % shape}
+        # the ISA these counters were taken on (the library the passes loaded): bench.py uses
+        # the figures only while its loaded library holds the same kernel bytes
+        sym = (kernel_hash.symbol('level', tile) if prefix == 'k_level1_mfq'
+               else kernel_hash.symbol('volume', tile, 2 if f16 else 4))
+        d['isa_symbol'] = sym
+        d['isa_sha16'] = kernel_hash.kernel_hash(sym) if sym else None
         if sq:
             t = sum(v[0] for v in sq.values()) / len(sq)
             grbm = mean(sq, 'GRBM_GUI_ACTIVE')

@@ -1,8 +1,9 @@
-"""Volume-kernel A/B timer: dm_corr_volume on the C3 batch (or --tiles of it), variants as
-env settings ("cs", "cs+DM_VOLUME_RB=2", "mfq+DM_VOLUME_CS=0"), interleaved rounds; --f16 times the
-binary16 volume (dm_corr_volume_f16).
+"""Volume-kernel timer: dm_corr_volume on the C3 batch (or --tiles of it), interleaved rounds;
+--f16 times the binary16 volume (dm_corr_volume_f16).  Library builds are A/B'd with
+DM_LIB_PATH (tools/ab3.sh); "+VAR=value" suffixes of a variant name set environment
+variables for that variant (none of the volume kernels reads one any more).
 
-    python tools/vbench.py [--variants cs,mfq+DM_VOLUME_CS=0] [--rounds 3] [--tiles 32]
+    python tools/vbench.py [--rounds 3] [--tiles 32] [--f16] [--mm]
 """
 import argparse
 import os
@@ -16,13 +17,12 @@ from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
 from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
-KNOBS = ('DM_VOLUME_CS', 'DM_VOLUME_RB', 'DM_VOLUME_NT', 'DM_VOLUME_LS', 'DM_VOLUME_MINW', 'DM_VOLUME_IMPL',
-         'DM_VOLUME_LSNW')
+KNOBS = ()
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--variants', default='cs')
+    ap.add_argument('--variants', default='ls')
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--tile', type=int, default=128)
     ap.add_argument('--tiles', type=int, default=32)
