@@ -715,8 +715,9 @@ def main():
                            'N_map = %d)' % (k, k, 2 ** (k - 1))}
 
     breakdown = split_breakdown(solver, rank, world, dev) if split else None
+    # (every rank decides alike: the re-solve below is collective for the c5 split)
     out_hash = step_check['sha256'] if step_check else None
-    if args.output_hash and out_hash is None:
+    if args.output_hash and step_check is None:
         res = solvers[0].step() if solvers else None    # split: every rank takes part
         torch.cuda.synchronize()
         if res is not None:

@@ -723,16 +723,18 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, in
 // time): the same expression as l0_value.
 template <int WS>
 struct PatchL0 {
-    static constexpr int NW4 = WS / 4 > 0 ? WS / 4 : 1, NR4 = WS % 4 > 0 ? WS % 4 : 1;
-    int Tw[WS][NW4]; // taps 4m..4m+3 of row u as packed signed bytes (v_dot4_i32_i8 operand)
-    int Tb[WS][NR4]; // the WS % 4 remaining taps of row u
+    // row u's taps as packed signed bytes (v_dot4_i32_i8 operands): NW4 full words of taps
+    // 4m..4m+3, then (WS % 4 != 0) one tail word with the WS % 4 remaining taps in its low
+    // bytes and zeros above -- the tail is one more dot4, not WS % 4 extract + multiply-adds
+    static constexpr int NW4 = WS / 4, NT = WS % 4 ? 1 : 0, NWD = NW4 + NT;
+    int Tw[WS][NWD];
     int sT;
     float ap, rmn, rmx;
     // tap k = T'[k / WS][k % WS] (k known at compile time after unrolling)
     __device__ int tap(int k) const
     {
         const int u = k / WS, v = k % WS;
-        return v < 4 * (WS / 4) ? ((int)((unsigned)Tw[u][v >> 2] << (24 - 8 * (v & 3)))) >> 24 : Tb[u][v - 4 * (WS / 4)];
+        return ((int)((unsigned)Tw[u][v >> 2] << (24 - 8 * (v & 3)))) >> 24;
     }
     __device__ void load(const Geo &g, const Stats &s, int t, int p0, int p1)
     {
@@ -744,14 +746,13 @@ struct PatchL0 {
 #pragma unroll
         for (int u = 0; u < WS; ++u) {
 #pragma unroll
-            for (int m = 0; m < WS / 4; ++m) {
+            for (int m = 0; m < NWD; ++m) {
                 unsigned w = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) w |= (unsigned)(T8[u * WS + 4 * m + k] & 0xFF) << (8 * k);
+                for (int k = 0; k < 4; ++k)
+                    if (4 * m + k < WS) w |= (unsigned)(T8[u * WS + 4 * m + k] & 0xFF) << (8 * k);
                 Tw[u][m] = (int)w;
             }
-#pragma unroll
-            for (int k = 0; k < WS % 4; ++k) Tb[u][k] = T8[u * WS + 4 * (WS / 4) + k];
         }
         const size_t op = (size_t)t * g.h0 * g.w0 + (size_t)p0 * g.w0 + p1;
         sT = s.sT[op]; ap = s.aP[op]; rmn = s.rmn[op]; rmx = s.rmx[op];
@@ -795,17 +796,13 @@ struct PatchL0 {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     int a = acc[i][j];
+                    // the tail word's zero taps meet bytes past the window (or E's zero pad)
 #pragma unroll
-                    for (int m = 0; m < WS / 4; ++m) {
+                    for (int m = 0; m < NWD; ++m) {
                         const int b0 = j + 4 * m;
                         const unsigned w = (b0 & 3) ? __builtin_amdgcn_alignbyte(E[(b0 >> 2) + 1], E[b0 >> 2], b0 & 3)
                                                     : E[b0 >> 2];
                         a = __builtin_amdgcn_sdot4(Tw[u][m], (int)w, a, false);
-                    }
-#pragma unroll
-                    for (int k = 0; k < WS % 4; ++k) {
-                        const int b = j + 4 * (WS / 4) + k;
-                        a += Tb[u][k] * (((int)(E[b >> 2] << (24 - 8 * (b & 3)))) >> 24);
                     }
                     acc[i][j] = a;
                 }
@@ -840,6 +837,17 @@ struct PatchL0 {
         return pow14((double)norm_x(r, rmn, rmx));
     }
 };
+
+// lane 4q + L of every quad (DPP quad_perm [L, L, L, L]), for a float64 value: two v_mov_dpp
+template <int L>
+__device__ __forceinline__ double quad_bcast(double v)
+{
+    constexpr int qp = L | (L << 2) | (L << 4) | (L << 6);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, qp, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), qp, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // The _B step onto level 1 when level 1 was never stored (dm_corr_level12 without level 1):
 // four lanes per entry, one per child patch of the level-1 cell.  A lane computes y on the
@@ -925,21 +933,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
             pool_row(i, yr);
         }
     }
+    // the 9 window sums: every lane of the entry's quad gets all four children (DPP quad
+    // broadcasts, in ul, ur, ll, lr order); lane ch then rectifies the sums of positions
+    // k = ch, ch + 4, ch + 8 only -- 3 sum pows per lane instead of 9 -- and lane 0 collects
+    // the window (out-of-range positions: 0, Matching's zero padding)
+    double mine[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const int a = k / 3, b = k % 3;
+        const int u = pd0 - 1 + a, v = pd1 - 1 + b;
+        double pv = 0.0;
+        const bool in = u >= 0 && u < h1 && v >= 0 && v < w1;
+        if (in) pv = pow14((double)norm_x(r_of_y(R[a][b], ap, g.method), rmn, rmx));
+        const double v0 = quad_bcast<0>(pv), v1 = quad_bcast<1>(pv), v2 = quad_bcast<2>(pv), v3 = quad_bcast<3>(pv);
+        if ((k & 3) == ch && in) mine[k >> 2] = pow14((((v0 + v1) + v2) + v3) / 4.0);
+    }
     double win[9];
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const int u = pd0 - 1 + a, v = pd1 - 1 + b;
-            double pv = 0.0;
-            const bool in = u >= 0 && u < h1 && v >= 0 && v < w1;
-            if (in) pv = pow14((double)norm_x(r_of_y(R[a][b], ap, g.method), rmn, rmx));
-            // children sum in ul, ur, ll, lr order (lanes 4e + 0..3)
-            const int base = (threadIdx.x & 63) & ~3;
-            const double v0 = __shfl(pv, base), v1 = __shfl(pv, base + 1), v2 = __shfl(pv, base + 2),
-                         v3 = __shfl(pv, base + 3);
-            win[a * 3 + b] = in ? pow14((((v0 + v1) + v2) + v3) / 4.0) : 0.0;
-        }
+    for (int k = 0; k < 9; ++k) {
+        const double m = mine[k >> 2];
+        win[k] = (k & 3) == 0 ? quad_bcast<0>(m) : (k & 3) == 1 ? quad_bcast<1>(m)
+                 : (k & 3) == 2 ? quad_bcast<2>(m) : quad_bcast<3>(m);
+    }
     if (!live || ch != 0) return;
     double o[3];
     near_pick(win, pd0, pd1, o);

@@ -625,7 +625,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             for (int r = 0; r < 4; ++r) { xch[sb][k][0][wc + 1][grp][r] = la[r]; xch[sb][k][1][wc + 1][grp][r] = lb[r]; }
             if (L2F && u > 0) xch2[sb][k ^ 1][wc][grp] = l1p[M - 1];
         }
-        __syncthreads();
+        // publishes the edge values to wave w+1; with one wave per cell block (NWc == 1: C2,
+        // NB = 2) no wave reads another's, and the blocks of a workgroup run unsynchronised
+        if constexpr (NWc > 1) __syncthreads();
         {
             // left neighbour of pooled column 0: lane c-1's last tile (DPP row_shr:1); lane
             // c == 0 keeps the DPP "old" operand = wave w-1's edge value (slot w; -inf for w = 0)
@@ -699,7 +701,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     if constexpr (L2F) {
         const int u = h0 / 2 - 1;
         if (NWc > 1 && c == 15) xch2[sb][u & 1][wc][grp] = l1p[M - 1];
-        __syncthreads();
+        if constexpr (NWc > 1) __syncthreads();
         level2_row(u, l1p);
     }
 }

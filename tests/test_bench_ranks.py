@@ -15,7 +15,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(*args, timeout=300):
+def _bench(*args, timeout=150):
     env = {k: v for k, v in os.environ.items()
            if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
     env.update(DM_BENCH_BACKEND='gloo', DM_BENCH_ONE_DEVICE='1', OMP_NUM_THREADS='4')

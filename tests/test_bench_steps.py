@@ -34,7 +34,7 @@ WS, GRID = 5, 8
 pytestmark = pytest.mark.gpu
 
 
-def _bench(*args, timeout=600):
+def _bench(*args, timeout=170):
     env = {k: v for k, v in os.environ.items()
            if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
     out = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--no-volume',

@@ -1,0 +1,31 @@
+#!/bin/bash
+# Ablation builds of the level kernel (timing upper bounds only; their results are WRONG):
+#   nobar   no barrier between the two waves of a workgroup in sweep 2 (dm_mfma.h:628)
+#   nopow   pow14_zf replaced by a widening multiply (the eight child pows per row pair)
+#   nosw1   sweep 1 (per-patch min / max) skipped
+# Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
+# travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
+set -euo pipefail
+REPO=$(cd "$(dirname "$0")/.." && pwd)
+FLAGS="-O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wno-pass-failed -mllvm -amdgpu-mfma-vgpr-form --offload-arch=gfx950"
+for v in "$@"; do
+  r=/tmp/abl_$v; rm -rf $r; d=$r/pkg; mkdir -p $d; cp -r $REPO/deepmatching_stereo_matching_amd/csrc $d/; cp -r $REPO/include $r/
+  case $v in
+    nobar) sed -i '628s/__syncthreads();/__builtin_amdgcn_wave_barrier();/' $d/csrc/dm_mfma.h ;;
+    nopow) python3 - $d/csrc/dm_kernels.hip <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+a = s.index('__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)\n{')
+b = s.index('\n}\n', a)
+s = s[:a] + '__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)\n{\n    return (double)x * 1.25;' + s[b:]
+open(p, 'w').write(s)
+PY
+    ;;
+    nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
+    base) ;;
+    *) echo "unknown $v"; exit 2 ;;
+  esac
+  (cd $d && /opt/rocm/bin/hipcc $FLAGS -I $r/include csrc/dm_kernels.hip csrc/dm_postproc.hip -o $REPO/ab/libdm_$v.so) &
+done
+wait
+ls -la $REPO/ab
