@@ -663,20 +663,25 @@ __device__ __forceinline__ void window_lvl(const double *M, int h, int w, int pd
         }
 }
 
-// top of the pyramid (_initial_move_map, :80-96): p_dot = p
-__global__ void k_match_top(const double *LK, int T, int h, int w, double *map)
+// top of the pyramid (_initial_move_map, :80-96): p_dot = p, for entry p of tile t
+__device__ __forceinline__ void match_top_at(const double *LK, int h, int w, size_t t, size_t p, double *map)
 {
-    DM_TAIL_ENTRY();
     const size_t P = (size_t)h * w;
-    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (idx >= (size_t)T * P) return;
-    const size_t t = idx / P, p = idx % P;
     const int i = (int)(p / w), j = (int)(p % w);
     double win[9], o[3];
     window_lvl(LK + (t * P + p) * P, h, w, i, j, win);
     near_pick(win, i, j, o);
     double *mt = map + t * 3 * P;
     mt[p] = o[0]; mt[P + p] = o[1]; mt[2 * P + p] = o[2];
+}
+
+__global__ void k_match_top(const double *LK, int T, int h, int w, double *map)
+{
+    DM_TAIL_ENTRY();
+    const size_t P = (size_t)h * w;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    match_top_at(LK, h, w, idx / P, idx % P, map);
 }
 
 __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r_)
@@ -687,16 +692,11 @@ __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r
 
 // one _B step (:98-139): parent map (h x w) -> child map (2h x 2w) on level L (materialised
 // when L != nullptr, else level lev = 0 or 1 on demand); at level 0 optionally _sub_pix_cal (:177-209)
-__global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, int h, int w,
-                             const double *pmap, double *cmap)
+__device__ __forceinline__ void match_step_at(const Geo &g, const Stats &s, const double *L, int lev, int h, int w,
+                                              int t, int pc, const double *pmap, double *cmap)
 {
-    DM_TAIL_ENTRY();
     const int hn = 2 * h, wn = 2 * w;
     const size_t P = (size_t)h * w, Pn = (size_t)hn * wn;
-    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (idx >= (size_t)T * Pn) return;
-    const int t = (int)(idx / Pn);
-    const int pc = (int)(idx % Pn);
     const int p0 = pc / wn, p1 = pc % wn;
     const int o0 = p0 & 1, o1 = p1 & 1;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
@@ -717,6 +717,16 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, in
     near_pick(win, pd0, pd1, o);
     double *cm_ = cmap + (size_t)t * 3 * Pn;
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
+}
+
+__global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, int h, int w,
+                             const double *pmap, double *cmap)
+{
+    DM_TAIL_ENTRY();
+    const size_t Pn = (size_t)(2 * h) * (2 * w);
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * Pn) return;
+    match_step_at(g, s, L, lev, h, w, (int)(idx / Pn), (int)(idx % Pn), pmap, cmap);
 }
 
 // Level-0 values of one patch on demand with its taps in registers (WS known at compile
@@ -855,20 +865,16 @@ __device__ __forceinline__ double quad_bcast(double v)
 // y (monotone: same as pooling the rectified values), normalises and rectifies the 9 pooled
 // values; the 4 lanes sum them in ul, ur, ll, lr order, /4, rectify -- the arithmetic of
 // k_level1_mfq / k_aggregate, so the window equals the stored level 1 bit for bit.
-template <int WS, int MW = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
+// Entry pc of tile t, child ch = lane & 3: the four lanes of a quad must run together (DPP);
+// a dead quad (live false) computes an entry of its tile and stores nothing.
+template <int WS>
+__device__ __forceinline__ void match_step_l1_at(const Geo &g, const Stats &s, int t, int pc, int ch, bool live,
+                                                 const double *pmap, double *cmap)
 {
-    DM_TAIL_ENTRY();
     constexpr int ws = WS, n = WS * WS;
     const int h0 = g.h0, w0 = g.w0;
     const int h1 = h0 / 2, w1 = w0 / 2, h = h1 / 2, w = w1 / 2;
     const size_t P = (size_t)h0 * w0, P1 = (size_t)h1 * w1, Pp = (size_t)h * w;
-    const size_t gid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t e = gid >> 2;
-    const int ch = (int)(gid & 3);
-    const bool live = e < (size_t)T * P1;
-    const size_t ee = live ? e : 0;
-    const int t = (int)(ee / P1), pc = (int)(ee % P1);
     const int p0 = pc / w1, p1 = pc % w1;
     const double *pm = pmap + (size_t)t * 3 * Pp;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
@@ -960,6 +966,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     near_pick(win, pd0, pd1, o);
     double *cm_ = cmap + (size_t)t * 3 * P1;
     cm_[pc] = o[0]; cm_[P1 + pc] = o[1]; cm_[2 * P1 + pc] = o[2];
+}
+
+template <int WS, int MW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l1(Geo g, Stats s, int T, const double *pmap, double *cmap)
+{
+    DM_TAIL_ENTRY();
+    const size_t P1 = (size_t)(g.h0 / 2) * (g.w0 / 2);
+    const size_t gid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t e = gid >> 2;
+    const bool live = e < (size_t)T * P1;
+    const size_t ee = live ? e : 0;
+    match_step_l1_at<WS>(g, s, (int)(ee / P1), (int)(ee % P1), (int)(gid & 3), live, pmap, cmap);
 }
 
 // Matching._sub_pix_cal (:177-209) on the final level-0 map, in place.  L0: materialised
@@ -1230,15 +1248,12 @@ static inline unsigned nblk(size_t n, unsigned bs)
 static constexpr unsigned TAIL_WG = 64u;
 
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
-template <int WS, int MW = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
+template <int WS>
+__device__ __forceinline__ void match_step_l0_at(const Geo &g, const Stats &s, int t, int pc, const double *pmap,
+                                                 double *cmap)
 {
-    DM_TAIL_ENTRY();
     const int hn = g.h0, wn = g.w0, h = hn / 2, w = wn / 2;
     const size_t Pp = (size_t)h * w, Pn = (size_t)hn * wn;
-    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (idx >= (size_t)T * Pn) return;
-    const int t = (int)(idx / Pn), pc = (int)(idx % Pn);
     const int p0 = pc / wn, p1 = pc % wn;
     const double *pm = pmap + (size_t)t * 3 * Pp;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
@@ -1273,16 +1288,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
 }
 
-// _sub_pix_cal with level 0 on demand, patch taps in registers (see k_subpix)
 template <int WS, int MW = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_subpix_t(Geo g, Stats s, int T, double *map)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_match_step_l0(Geo g, Stats s, int T, const double *pmap, double *cmap)
 {
     DM_TAIL_ENTRY();
+    const size_t Pn = (size_t)g.h0 * g.w0;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * Pn) return;
+    match_step_l0_at<WS>(g, s, (int)(idx / Pn), (int)(idx % Pn), pmap, cmap);
+}
+
+// _sub_pix_cal with level 0 on demand, patch taps in registers (see k_subpix)
+template <int WS>
+__device__ __forceinline__ void subpix_at(const Geo &g, const Stats &s, int t, int pc, double *map)
+{
     const int h0 = g.h0, w0 = g.w0;
     const size_t P = (size_t)h0 * w0;
-    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (idx >= (size_t)T * P) return;
-    const int t = (int)(idx / P), pc = (int)(idx % P);
     const int p0 = pc / w0, p1 = pc % w0;
     double *mt = map + (size_t)t * 3 * P;
     PatchL0<WS> pt;
@@ -1321,6 +1342,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     }
     mt[pc] = nrow;
     mt[P + pc] = ncol;
+}
+
+template <int WS, int MW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void k_subpix_t(Geo g, Stats s, int T, double *map)
+{
+    DM_TAIL_ENTRY();
+    const size_t P = (size_t)g.h0 * g.w0;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (idx >= (size_t)T * P) return;
+    subpix_at<WS>(g, s, (int)(idx / P), (int)(idx % P), map);
+}
+
+// ------------------------------------------------------------------------------------
+// The whole descent of dm_match for ONE tile per workgroup, in one launch: the top of the
+// pyramid, the _B steps on the stored levels K-1 .. 2, the steps onto level 1 and level 0 on
+// demand and the sub-pixel pass (Matching.py:80-209), each phase looping over the tile's
+// entries with the workgroup and separated by a workgroup barrier -- the same per-entry
+// device functions as the per-level kernels, so the maps are bit-identical.  A tile's
+// descent depends on that tile's pyramid only (image_cut_solver.py:115-142), so no other
+// synchronisation is needed.  Beside the next pair's level kernel this is one launch of T
+// workgroups that dispatch as soon as CUs free up, instead of ~10 dependent launches that
+// each wait for the level kernel's waves to drain.
+// Buffers alternate between b0 and b1 per phase (maps [T][3][h][w] of each level); the
+// caller picks them so that the last phase lands in the output.
+#define TC_THREADS 512
+template <int WS>
+__global__ __launch_bounds__(TC_THREADS) void k_tile_chain(Geo g, Stats s, Levels lv, int nlev, int sub_pix,
+                                                        double *b0, double *b1)
+{
+    DM_TAIL_ENTRY();
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int K = nlev - 1;
+    int h = g.h0 >> K, w = g.w0 >> K;
+    double *cur = b0, *nxt = b1;
+    for (int p = tid; p < h * w; p += TC_THREADS) match_top_at(lv.lv[K], h, w, t, p, cur);
+    for (int l = K - 1; l >= 0; --l) {
+        __syncthreads();
+        const int n = (2 * h) * (2 * w);
+        if (l == 0 && !lv.lv[0]) {
+            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_l0_at<WS>(g, s, t, pc, cur, nxt);
+        } else if (l == 1 && !lv.lv[1]) {
+            // four lanes (one quad) per entry: TC_THREADS % 4 == 0 and 4 n % 4 == 0, so a
+            // quad's lanes are live together
+            for (int i = tid; i < 4 * n; i += TC_THREADS) match_step_l1_at<WS>(g, s, t, i >> 2, i & 3, true, cur, nxt);
+        } else {
+            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_at(g, s, lv.lv[l], l, h, w, t, pc, cur, nxt);
+        }
+        double *x = cur; cur = nxt; nxt = x;
+        h *= 2; w *= 2;
+    }
+    if (sub_pix) {
+        __syncthreads();
+        for (int pc = tid; pc < h * w; pc += TC_THREADS) subpix_at<WS>(g, s, t, pc, cur);
+    }
 }
 
 template <int WS>
@@ -1444,7 +1519,7 @@ static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, O
 
 extern "C" {
 
-int dm_abi_version(void) { return 107; }
+int dm_abi_version(void) { return 108; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1659,6 +1734,17 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
              int32_t T, int32_t h0, int32_t w0, int32_t sub_pix, int32_t filter_window,
              int32_t filter_num, int32_t filter_mode, double *d_scratch, double *d_out, void *stream)
 {
+    return dm_match_ex(b, d_stats, d_levels, nlev, T, h0, w0, sub_pix, filter_window, filter_num, filter_mode,
+                       DM_MATCH_AUTO, d_scratch, d_out, stream);
+}
+
+int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_levels, int32_t nlev,
+                int32_t T, int32_t h0, int32_t w0, int32_t sub_pix, int32_t filter_window,
+                int32_t filter_num, int32_t filter_mode, int32_t schedule, double *d_scratch, double *d_out,
+                void *stream)
+{
+    if (schedule != DM_MATCH_AUTO && schedule != DM_MATCH_PER_LEVEL && schedule != DM_MATCH_PER_TILE)
+        return fail(DM_ERR_ARG, "unknown matching schedule %d", schedule);
     if (!d_levels || !d_scratch || !d_out) return fail(DM_ERR_ARG, "null pointer");
     if (T < 1 || h0 < 1 || w0 < 1) return fail(DM_ERR_ARG, "empty batch (T=%d, h0=%d, w0=%d)", T, h0, w0);
     if (nlev < 2) return fail(DM_ERR_SHAPE, "list index out of range: Matching._B needs >= 2 levels (got %d)", nlev);
@@ -1683,8 +1769,36 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
         s = stats_view((void *)d_stats, T, h0 * w0);
     }
     hipStream_t st = (hipStream_t)stream;
+    // per-tile schedule: the whole descent in one launch of T workgroups (k_tile_chain), for
+    // level 0 on demand, no filter and ws = 5; AUTO takes it from 16 tiles up (below that a
+    // per-level launch spreads one tile's entries over more of the chip)
+    const bool tile_ok = !d_levels[0] && filter_num <= 0 && g.ws == 5;
+    if (schedule == DM_MATCH_PER_TILE && !tile_ok)
+        return fail(DM_ERR_UNSUPPORTED, "per-tile matching needs level 0 on demand, no filter and ws = 5");
+    if (tile_ok && (schedule == DM_MATCH_PER_TILE || (schedule == DM_MATCH_AUTO && T >= 16))) {
+        Levels lv{};
+        for (int l = 0; l < nlev; ++l) lv.lv[l] = d_levels[l];
+        // K phases swap the buffers: start so that the last one writes d_out
+        double *b0 = (K & 1) ? d_scratch : d_out, *b1 = (K & 1) ? d_out : d_scratch;
+        k_tile_chain<5><<<T, TC_THREADS, 0, st>>>(g, s, lv, nlev, sub_pix, b0, b1);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
+    // per-level schedule: one launch per phase; the buffer parity is chosen so that the last
+    // phase writes d_out (no copy): count the swaps (K steps + the filter passes that run)
+    int swaps = K;
+    {
+        int fl = filter_num, hh = h0 >> K, ww = w0 >> K;
+        for (int l = K; l >= 0; --l) {
+            if (fl > 0) {
+                if (hh >= filter_window && ww >= filter_window) ++swaps;
+                --fl;
+            }
+            hh *= 2; ww *= 2;
+        }
+    }
     double *buf[2] = {d_out, d_scratch};
-    int cur = 0;
+    int cur = swaps & 1;
     int h = h0 >> K, w = w0 >> K;
     int fleft = filter_num;
     auto filt = [&](int hh, int ww) -> int { // Matching._filter hook (:91-93, :136-138)
@@ -1758,7 +1872,7 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
         }
         HIP_TRY(hipGetLastError());
     }
-    if (buf[cur] != d_out)
+    if (buf[cur] != d_out) // (the parity above makes this unreachable; kept as a guard)
         HIP_TRY(hipMemcpyAsync(d_out, buf[cur], sizeof(double) * 3 * (size_t)T * h0 * w0, hipMemcpyDeviceToDevice, st));
     return DM_OK;
 }

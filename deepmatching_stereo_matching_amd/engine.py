@@ -326,13 +326,15 @@ class DevicePyramid:
         return out
 
     def match(self, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
-              filtering_mode='median', levels=None, nlev=None):
+              filtering_mode='median', levels=None, nlev=None, schedule=L.DM_MATCH_AUTO):
         """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score).
         ``levels``: an explicit co_map_list (e.g. materialized_levels()) to match on
         instead of this pyramid's (level 0 then read from memory, not re-derived).
         ``nlev``: match on the first ``nlev`` levels only, the reference's Matching on a
         co_map_list cut to k levels with N_map = 2^(k-1): the descent
-        starts at level nlev - 1, one start per cell of that level (Matching.py:80-96)."""
+        starts at level nlev - 1, one start per cell of that level (Matching.py:80-96).
+        ``schedule``: dm_match_ex's launch schedule (one launch per phase, or the whole
+        descent in one launch with a workgroup per tile); the results are the same."""
         b = self.b
         n = self.nlev if nlev is None else int(nlev)
         if not 1 <= n <= self.nlev:
@@ -352,10 +354,10 @@ class DevicePyramid:
             ptrs = (ctypes.c_void_p * n)(*([None] + [None if t is None else t.data_ptr()
                                                       for t in self.levels[1:n]]))
         fnum = int(filtering_num) if filtering else 0
-        L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, n, b.T, b.h0, b.w0,
-                                  int(bool(sub_pix)), int(filter_window_size), fnum,
-                                  1 if filtering_mode == 'median' else 0,
-                                  L.ptr(scratch), L.ptr(out), self._s()), 'dm_match')
+        L.check(self.lib.dm_match_ex(b.ref(), L.ptr(self.stats), ptrs, n, b.T, b.h0, b.w0,
+                                     int(bool(sub_pix)), int(filter_window_size), fnum,
+                                     1 if filtering_mode == 'median' else 0, int(schedule),
+                                     L.ptr(scratch), L.ptr(out), self._s()), 'dm_match_ex')
         return out
 
 
