@@ -527,34 +527,39 @@ __global__ __launch_bounds__(256) void k_pow_variant(const double *in, size_t n,
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ double nanmax(double acc, double v) { return (v > acc || isnan(v)) ? v : acc; }
 
+// one output value of the aggregation step: tile t, rem = cell * P2 + position
+__device__ __forceinline__ void aggregate_at(const double *in, int h, int w, int rectify, size_t t, size_t rem,
+                                             double *out)
+{
+    const int h2 = h / 2, w2 = w / 2;
+    const size_t P = (size_t)h * w, P2 = (size_t)h2 * w2;
+    const int cell = (int)(rem / P2), k = (int)(rem % P2);
+    const int I = cell / w2, J = cell % w2, u = k / w2, v = k % w2;
+    double acc = 0.0;
+    for (int ch = 0; ch < 4; ++ch) {
+        const int c = (2 * I + (ch >> 1)) * w + 2 * J + (ch & 1);
+        const double *m = in + (t * P + c) * P;
+        double mx = -INFINITY;
+        for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
+            if (a < 0 || a >= h) continue;
+            for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
+                if (b < 0 || b >= w) continue;
+                mx = nanmax(mx, m[(size_t)a * w + b]);
+            }
+        }
+        acc = ch == 0 ? mx : acc + mx;
+    }
+    out[t * P2 * P2 + rem] = rectify ? pow14(acc / 4.0) : acc / 4.0;
+}
+
 __global__ void k_aggregate(const double *in, int T, int h, int w, int rectify, double *out)
 {
     DM_TAIL_ENTRY();
-    const int h2 = h / 2, w2 = w / 2;
-    const size_t P = (size_t)h * w, P2 = (size_t)h2 * w2;
+    const size_t P2 = (size_t)(h / 2) * (w / 2);
     const size_t total = (size_t)T * P2 * P2;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * blockDim.x) {
-        const size_t t = idx / (P2 * P2);
-        const size_t rem = idx % (P2 * P2);
-        const int cell = (int)(rem / P2), k = (int)(rem % P2);
-        const int I = cell / w2, J = cell % w2, u = k / w2, v = k % w2;
-        double acc = 0.0;
-        for (int ch = 0; ch < 4; ++ch) {
-            const int c = (2 * I + (ch >> 1)) * w + 2 * J + (ch & 1);
-            const double *m = in + (t * P + c) * P;
-            double mx = -INFINITY;
-            for (int a = 2 * u - 1; a <= 2 * u + 1; ++a) {
-                if (a < 0 || a >= h) continue;
-                for (int b = 2 * v - 1; b <= 2 * v + 1; ++b) {
-                    if (b < 0 || b >= w) continue;
-                    mx = nanmax(mx, m[(size_t)a * w + b]);
-                }
-            }
-            acc = ch == 0 ? mx : acc + mx;
-        }
-        out[idx] = rectify ? pow14(acc / 4.0) : acc / 4.0;
-    }
+         idx += (size_t)gridDim.x * blockDim.x)
+        aggregate_at(in, h, w, rectify, idx / (P2 * P2), idx % (P2 * P2), out);
 }
 
 // Same result as k_aggregate, streaming: one workgroup per (tile, output cell, band of
@@ -664,14 +669,17 @@ __device__ __forceinline__ void window_lvl(const double *M, int h, int w, int pd
 }
 
 // top of the pyramid (_initial_move_map, :80-96): p_dot = p, for entry p of tile t
-__device__ __forceinline__ void match_top_at(const double *LK, int h, int w, size_t t, size_t p, double *map)
+// Map buffers of the matching phases hold one (3, h, w) map per tile: tile t's at
+// map + t * ms, ms = 3 h w for the per-level launches (maps packed per level) and 3 h0 w0 for
+// k_tile_chain (a fixed region per tile: its tiles run different levels at once).
+__device__ __forceinline__ void match_top_at(const double *LK, int h, int w, size_t t, size_t p, double *map, size_t ms)
 {
     const size_t P = (size_t)h * w;
     const int i = (int)(p / w), j = (int)(p % w);
     double win[9], o[3];
     window_lvl(LK + (t * P + p) * P, h, w, i, j, win);
     near_pick(win, i, j, o);
-    double *mt = map + t * 3 * P;
+    double *mt = map + t * ms;
     mt[p] = o[0]; mt[P + p] = o[1]; mt[2 * P + p] = o[2];
 }
 
@@ -681,7 +689,7 @@ __global__ void k_match_top(const double *LK, int T, int h, int w, double *map)
     const size_t P = (size_t)h * w;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
-    match_top_at(LK, h, w, idx / P, idx % P, map);
+    match_top_at(LK, h, w, idx / P, idx % P, map, 3 * P);
 }
 
 __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r_)
@@ -693,14 +701,14 @@ __device__ __forceinline__ double sub_pix_compute(double r0, double r1, double r
 // one _B step (:98-139): parent map (h x w) -> child map (2h x 2w) on level L (materialised
 // when L != nullptr, else level lev = 0 or 1 on demand); at level 0 optionally _sub_pix_cal (:177-209)
 __device__ __forceinline__ void match_step_at(const Geo &g, const Stats &s, const double *L, int lev, int h, int w,
-                                              int t, int pc, const double *pmap, double *cmap)
+                                              int t, int pc, const double *pmap, size_t pms, double *cmap, size_t cms)
 {
     const int hn = 2 * h, wn = 2 * w;
     const size_t P = (size_t)h * w, Pn = (size_t)hn * wn;
     const int p0 = pc / wn, p1 = pc % wn;
     const int o0 = p0 & 1, o1 = p1 & 1;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
-    const double *pm = pmap + (size_t)t * 3 * P;
+    const double *pm = pmap + (size_t)t * pms;
     const int pd0 = (int)(long long)(pm[par] * 2) + o0;
     const int pd1 = (int)(long long)(pm[P + par] * 2) + o1;
     double win[9], o[3];
@@ -715,7 +723,7 @@ __device__ __forceinline__ void match_step_at(const Geo &g, const Stats &s, cons
             }
     }
     near_pick(win, pd0, pd1, o);
-    double *cm_ = cmap + (size_t)t * 3 * Pn;
+    double *cm_ = cmap + (size_t)t * cms;
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
 }
 
@@ -726,7 +734,7 @@ __global__ void k_match_step(Geo g, Stats s, const double *L, int lev, int T, in
     const size_t Pn = (size_t)(2 * h) * (2 * w);
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * Pn) return;
-    match_step_at(g, s, L, lev, h, w, (int)(idx / Pn), (int)(idx % Pn), pmap, cmap);
+    match_step_at(g, s, L, lev, h, w, (int)(idx / Pn), (int)(idx % Pn), pmap, 3 * (size_t)h * w, cmap, 3 * Pn);
 }
 
 // Level-0 values of one patch on demand with its taps in registers (WS known at compile
@@ -869,14 +877,14 @@ __device__ __forceinline__ double quad_bcast(double v)
 // a dead quad (live false) computes an entry of its tile and stores nothing.
 template <int WS>
 __device__ __forceinline__ void match_step_l1_at(const Geo &g, const Stats &s, int t, int pc, int ch, bool live,
-                                                 const double *pmap, double *cmap)
+                                                 const double *pmap, size_t pms, double *cmap, size_t cms)
 {
     constexpr int ws = WS, n = WS * WS;
     const int h0 = g.h0, w0 = g.w0;
     const int h1 = h0 / 2, w1 = w0 / 2, h = h1 / 2, w = w1 / 2;
     const size_t P = (size_t)h0 * w0, P1 = (size_t)h1 * w1, Pp = (size_t)h * w;
     const int p0 = pc / w1, p1 = pc % w1;
-    const double *pm = pmap + (size_t)t * 3 * Pp;
+    const double *pm = pmap + (size_t)t * pms;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
     const int pd0 = (int)(long long)(pm[par] * 2) + (p0 & 1);
     const int pd1 = (int)(long long)(pm[Pp + par] * 2) + (p1 & 1);
@@ -964,7 +972,7 @@ __device__ __forceinline__ void match_step_l1_at(const Geo &g, const Stats &s, i
     if (!live || ch != 0) return;
     double o[3];
     near_pick(win, pd0, pd1, o);
-    double *cm_ = cmap + (size_t)t * 3 * P1;
+    double *cm_ = cmap + (size_t)t * cms;
     cm_[pc] = o[0]; cm_[P1 + pc] = o[1]; cm_[2 * P1 + pc] = o[2];
 }
 
@@ -977,7 +985,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     const size_t e = gid >> 2;
     const bool live = e < (size_t)T * P1;
     const size_t ee = live ? e : 0;
-    match_step_l1_at<WS>(g, s, (int)(ee / P1), (int)(ee % P1), (int)(gid & 3), live, pmap, cmap);
+    match_step_l1_at<WS>(g, s, (int)(ee / P1), (int)(ee % P1), (int)(gid & 3), live, pmap, 3 * (P1 / 4), cmap, 3 * P1);
 }
 
 // Matching._sub_pix_cal (:177-209) on the final level-0 map, in place.  L0: materialised
@@ -1250,12 +1258,12 @@ static constexpr unsigned TAIL_WG = 64u;
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
 template <int WS>
 __device__ __forceinline__ void match_step_l0_at(const Geo &g, const Stats &s, int t, int pc, const double *pmap,
-                                                 double *cmap)
+                                                 size_t pms, double *cmap, size_t cms)
 {
     const int hn = g.h0, wn = g.w0, h = hn / 2, w = wn / 2;
     const size_t Pp = (size_t)h * w, Pn = (size_t)hn * wn;
     const int p0 = pc / wn, p1 = pc % wn;
-    const double *pm = pmap + (size_t)t * 3 * Pp;
+    const double *pm = pmap + (size_t)t * pms;
     const size_t par = (size_t)(p0 >> 1) * w + (p1 >> 1);
     const int pd0 = (int)(long long)(pm[par] * 2) + (p0 & 1);
     const int pd1 = (int)(long long)(pm[Pp + par] * 2) + (p1 & 1);
@@ -1284,7 +1292,7 @@ __device__ __forceinline__ void match_step_l0_at(const Geo &g, const Stats &s, i
             }
     }
     near_pick(win, pd0, pd1, o);
-    double *cm_ = cmap + (size_t)t * 3 * Pn;
+    double *cm_ = cmap + (size_t)t * cms;
     cm_[pc] = o[0]; cm_[Pn + pc] = o[1]; cm_[2 * Pn + pc] = o[2];
 }
 
@@ -1295,17 +1303,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     const size_t Pn = (size_t)g.h0 * g.w0;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * Pn) return;
-    match_step_l0_at<WS>(g, s, (int)(idx / Pn), (int)(idx % Pn), pmap, cmap);
+    match_step_l0_at<WS>(g, s, (int)(idx / Pn), (int)(idx % Pn), pmap, 3 * (Pn / 4), cmap, 3 * Pn);
 }
 
 // _sub_pix_cal with level 0 on demand, patch taps in registers (see k_subpix)
 template <int WS>
-__device__ __forceinline__ void subpix_at(const Geo &g, const Stats &s, int t, int pc, double *map)
+__device__ __forceinline__ void subpix_at(const Geo &g, const Stats &s, int t, int pc, double *map, size_t ms)
 {
     const int h0 = g.h0, w0 = g.w0;
     const size_t P = (size_t)h0 * w0;
     const int p0 = pc / w0, p1 = pc % w0;
-    double *mt = map + (size_t)t * 3 * P;
+    double *mt = map + (size_t)t * ms;
     PatchL0<WS> pt;
     pt.load(g, s, t, p0, p1);
     const double row = mt[pc], col = mt[P + pc];
@@ -1351,7 +1359,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     const size_t P = (size_t)g.h0 * g.w0;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (idx >= (size_t)T * P) return;
-    subpix_at<WS>(g, s, (int)(idx / P), (int)(idx % P), map);
+    subpix_at<WS>(g, s, (int)(idx / P), (int)(idx % P), map, 3 * P);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1364,37 +1372,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
 // synchronisation is needed.  Beside the next pair's level kernel this is one launch of T
 // workgroups that dispatch as soon as CUs free up, instead of ~10 dependent launches that
 // each wait for the level kernel's waves to drain.
-// Buffers alternate between b0 and b1 per phase (maps [T][3][h][w] of each level); the
-// caller picks them so that the last phase lands in the output.
+// Buffers alternate between b0 and b1 per phase; tile t's maps of every level live in its own
+// region t * 3 h0 w0 of them (its tiles run different levels at once, so the per-level
+// packing [T][3][h][w] of the per-level launches would let them overwrite each other), which
+// at level 0 is the packed [T][3][h0][w0] output.  The caller picks the buffers so that the
+// last phase lands in the output.
 #define TC_THREADS 512
+// build_from > 0: levels build_from + 1 .. K are first built from level build_from (the
+// pyramid's aggregation steps, Correlation_map.py:89-130 + :148, for this tile: aggregate_at,
+// k_aggregate's arithmetic) into lv's buffers -- the tile's levels depend on its own only.
 template <int WS>
-__global__ __launch_bounds__(TC_THREADS) void k_tile_chain(Geo g, Stats s, Levels lv, int nlev, int sub_pix,
-                                                        double *b0, double *b1)
+__global__ __launch_bounds__(TC_THREADS) void k_tile_chain(Geo g, Stats s, Levels lv, int nlev, int build_from,
+                                                        int sub_pix, double *b0, double *b1)
 {
     DM_TAIL_ENTRY();
     const int t = blockIdx.x, tid = threadIdx.x;
     const int K = nlev - 1;
+    if (build_from > 0) {
+        for (int l = build_from + 1; l <= K; ++l) {
+            const int hp = g.h0 >> (l - 1), wp = g.w0 >> (l - 1);
+            const size_t n2 = (size_t)(hp / 2) * (wp / 2);
+            for (size_t i = tid; i < n2 * n2; i += TC_THREADS) aggregate_at(lv.lv[l - 1], hp, wp, 1, t, i, (double *)lv.lv[l]);
+            __syncthreads();
+        }
+    }
     int h = g.h0 >> K, w = g.w0 >> K;
     double *cur = b0, *nxt = b1;
-    for (int p = tid; p < h * w; p += TC_THREADS) match_top_at(lv.lv[K], h, w, t, p, cur);
+    const size_t ms = 3 * (size_t)g.h0 * g.w0;   // tile t's region in b0 / b1, every level
+    for (int p = tid; p < h * w; p += TC_THREADS) match_top_at(lv.lv[K], h, w, t, p, cur, ms);
     for (int l = K - 1; l >= 0; --l) {
         __syncthreads();
         const int n = (2 * h) * (2 * w);
         if (l == 0 && !lv.lv[0]) {
-            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_l0_at<WS>(g, s, t, pc, cur, nxt);
+            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_l0_at<WS>(g, s, t, pc, cur, ms, nxt, ms);
         } else if (l == 1 && !lv.lv[1]) {
             // four lanes (one quad) per entry: TC_THREADS % 4 == 0 and 4 n % 4 == 0, so a
             // quad's lanes are live together
-            for (int i = tid; i < 4 * n; i += TC_THREADS) match_step_l1_at<WS>(g, s, t, i >> 2, i & 3, true, cur, nxt);
+            for (int i = tid; i < 4 * n; i += TC_THREADS)
+                match_step_l1_at<WS>(g, s, t, i >> 2, i & 3, true, cur, ms, nxt, ms);
         } else {
-            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_at(g, s, lv.lv[l], l, h, w, t, pc, cur, nxt);
+            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_at(g, s, lv.lv[l], l, h, w, t, pc, cur, ms, nxt, ms);
         }
         double *x = cur; cur = nxt; nxt = x;
         h *= 2; w *= 2;
     }
     if (sub_pix) {
         __syncthreads();
-        for (int pc = tid; pc < h * w; pc += TC_THREADS) subpix_at<WS>(g, s, t, pc, cur);
+        for (int pc = tid; pc < h * w; pc += TC_THREADS) subpix_at<WS>(g, s, t, pc, cur, ms);
     }
 }
 
@@ -1743,7 +1767,9 @@ int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_l
                 int32_t filter_num, int32_t filter_mode, int32_t schedule, double *d_scratch, double *d_out,
                 void *stream)
 {
-    if (schedule != DM_MATCH_AUTO && schedule != DM_MATCH_PER_LEVEL && schedule != DM_MATCH_PER_TILE)
+    const int sched = schedule & 3;
+    const bool build_upper = (schedule & DM_MATCH_BUILD_UPPER) != 0;
+    if ((schedule & ~(3 | DM_MATCH_BUILD_UPPER)) || sched == 3 || (build_upper && sched == DM_MATCH_PER_LEVEL))
         return fail(DM_ERR_ARG, "unknown matching schedule %d", schedule);
     if (!d_levels || !d_scratch || !d_out) return fail(DM_ERR_ARG, "null pointer");
     if (T < 1 || h0 < 1 || w0 < 1) return fail(DM_ERR_ARG, "empty batch (T=%d, h0=%d, w0=%d)", T, h0, w0);
@@ -1773,14 +1799,16 @@ int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_l
     // level 0 on demand, no filter and ws = 5; AUTO takes it from 16 tiles up (below that a
     // per-level launch spreads one tile's entries over more of the chip)
     const bool tile_ok = !d_levels[0] && filter_num <= 0 && g.ws == 5;
-    if (schedule == DM_MATCH_PER_TILE && !tile_ok)
+    if ((sched == DM_MATCH_PER_TILE || build_upper) && !tile_ok)
         return fail(DM_ERR_UNSUPPORTED, "per-tile matching needs level 0 on demand, no filter and ws = 5");
-    if (tile_ok && (schedule == DM_MATCH_PER_TILE || (schedule == DM_MATCH_AUTO && T >= 16))) {
+    if (build_upper && (nlev < 4 || !d_levels[2]))
+        return fail(DM_ERR_ARG, "DM_MATCH_BUILD_UPPER builds levels 3.. from a stored level 2 (nlev >= 4)");
+    if (tile_ok && (sched == DM_MATCH_PER_TILE || build_upper || (sched == DM_MATCH_AUTO && T >= 16))) {
         Levels lv{};
         for (int l = 0; l < nlev; ++l) lv.lv[l] = d_levels[l];
         // K phases swap the buffers: start so that the last one writes d_out
         double *b0 = (K & 1) ? d_scratch : d_out, *b1 = (K & 1) ? d_out : d_scratch;
-        k_tile_chain<5><<<T, TC_THREADS, 0, st>>>(g, s, lv, nlev, sub_pix, b0, b1);
+        k_tile_chain<5><<<T, TC_THREADS, 0, st>>>(g, s, lv, nlev, build_upper ? 2 : 0, sub_pix, b0, b1);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }

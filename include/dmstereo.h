@@ -179,8 +179,12 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
  *                       demand, no filter, ws = 5; DM_ERR_UNSUPPORTED otherwise): a pipelined
  *                       caller's tail is then one launch that runs beside the next pair's level
  *                       kernel instead of ~10 dependent ones waiting for it to drain;
- *   DM_MATCH_AUTO       PER_TILE where it applies and T >= 16, else PER_LEVEL (= dm_match). */
-enum dm_match_schedule { DM_MATCH_AUTO = 0, DM_MATCH_PER_LEVEL = 1, DM_MATCH_PER_TILE = 2 };
+ *   DM_MATCH_AUTO       PER_TILE where it applies and T >= 16, else PER_LEVEL (= dm_match).
+ * | DM_MATCH_BUILD_UPPER (per-tile only): d_levels[3 .. nlev-1] are OUTPUT buffers, built in
+ *   the same launch from the stored level 2 (dm_aggregate's arithmetic, rectify on) before
+ *   the descent -- the pyramid's last aggregation steps join the one-launch tail. */
+enum dm_match_schedule { DM_MATCH_AUTO = 0, DM_MATCH_PER_LEVEL = 1, DM_MATCH_PER_TILE = 2,
+                         DM_MATCH_BUILD_UPPER = 4 };
 int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_levels,
                 int32_t nlev, int32_t T, int32_t h0, int32_t w0, int32_t sub_pix,
                 int32_t filter_window, int32_t filter_num, int32_t filter_mode, int32_t schedule,

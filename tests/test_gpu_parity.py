@@ -610,3 +610,34 @@ def test_match_per_tile_unsupported_cases():
         p3.match(schedule=7)
     # the per-level schedule still takes both
     _same(p3.match(schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy(), p3.match().cpu().numpy())
+
+
+@pytest.mark.parametrize('S,T,nlev', [(32, 18, None), (64, 16, None), (64, 16, 4), (128, 16, 5)])
+def test_match_builds_upper_levels(S, T, nlev):
+    """build(defer_upper=True) + match(): levels 3.. are built inside the per-tile matching
+    launch (DM_MATCH_BUILD_UPPER); levels, maps and sub-pixel equal the eager dm_aggregate
+    build + per-level matching bit for bit, and a later read of a deferred level is correct."""
+    from deepmatching_stereo_matching_amd import _lib as L
+    from deepmatching_stereo_matching_amd import engine
+    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
+    side = S + 4
+    a, b = stereo_pair(side + 2 * T, side + 3, seed=3 * S + T, dx=2, sinusoidal=True)
+    a[7:7 + 6, 9:9 + 5] = 200
+    org = [(2 * t, t % 4) for t in range(T)]
+    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
+    ref.build(nlev=nlev)
+    want = ref.match(nlev=nlev, schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy()
+    top = ref.nlev if nlev is None else nlev
+    pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
+    pyr.build(nlev=nlev, defer_upper=True)
+    assert pyr._pending_upper == (top >= 4)
+    _same(pyr.match(nlev=nlev).cpu().numpy(), want)
+    assert not pyr._pending_upper
+    for k in range(3, top):
+        _same(pyr.levels[k].cpu().numpy(), ref.levels[k].cpu().numpy())
+    # a deferred level read before any match is built on demand
+    lazy = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
+    lazy.build(nlev=nlev, defer_upper=True)
+    if top >= 4:
+        _same(lazy.level(top - 1).cpu().numpy(), ref.levels[top - 1].cpu().numpy())
+        _same(lazy.match(nlev=nlev, schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy(), want)
