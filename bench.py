@@ -57,8 +57,7 @@ S = 128
 GRID = 8
 CONFIGS = {'c2': (64, 8), 'c3': (128, 8), 'c4': (128, 8), 'c5': (256, 16)}   # (tile S, tiles per axis)
 C4_PAIRS = 64                  # BASELINE configs[3]: a batch of 64 independent 1024^2 pairs
-BASELINE_LEVELS = {'c2': 3, 'c3': 4, 'c4': 4}
-SCHEDULES = {'auto': L.DM_MATCH_AUTO, 'level': L.DM_MATCH_PER_LEVEL, 'tile': L.DM_MATCH_PER_TILE}   # BASELINE configs[1..3]: "3-level" / "4-level pyramid"
+BASELINE_LEVELS = {'c2': 3, 'c3': 4, 'c4': 4}   # BASELINE configs[1..3]: "3-level" / "4-level pyramid"
 SPEC_CLOCK_GHZ = 2.4           # MI355X_MICROARCH.md: max clock (the issue roofline's peak)
 # Rehearsal of the multi-rank path on a box with fewer GPUs than ranks (tests/test_bench_ranks.py):
 # DM_BENCH_BACKEND=gloo and DM_BENCH_ONE_DEVICE=1 put every rank on cuda:0 over gloo.  The
@@ -109,10 +108,6 @@ def parse():
     ap.add_argument('--no-c5-split', action='store_true',
                     help='c3: skip the c5_split sub-line (one 4096^2 pair, tiles split over the ranks)')
     ap.add_argument('--c5-steps', type=int, default=3, help='timed steps of the c5_split sub-line')
-    ap.add_argument('--match-schedule', choices=('auto', 'level', 'tile'), default='auto',
-                    help="dm_match_ex's launch schedule: one launch per phase ('level'), the whole "
-                         "descent in one launch of a workgroup per tile ('tile'), or 'auto' (tile "
-                         "from 16 tiles up)")
     return ap.parse_args()
 
 
@@ -120,7 +115,7 @@ class PairSolver:
     """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
     dominant kernel (dm_corr_level12)."""
 
-    def __init__(self, img1, img2, tile, grid, split=False, levels=None, schedule=L.DM_MATCH_AUTO):
+    def __init__(self, img1, img2, tile, grid, split=False, levels=None):
         """split: the pair's tiles are sharded over the ranks (rank r solves tiles r::N) and
         the per-tile results are gathered to rank 0 (RCCL over xGMI), which stitches the map;
         otherwise this rank solves every tile of its own pair.  levels: k-level pyramid
@@ -137,7 +132,6 @@ class PairSolver:
         self.batch = engine.TileBatch(img1, img2, self.origins, tile, tile, WS,
                                       L.DM_TM_CCOEFF_NORMED, self.dev)
         self.ev = []
-        self.schedule = schedule
 
     def step(self, timed=False, stream=None, wait=None, level_stream=None, stats_stream=None):
         """One full solve of the pair on `stream` (default: the current stream).  Every
@@ -168,13 +162,10 @@ class PairSolver:
             self.ev.append(ev)
         self.last_end = ev[1]
         diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
-        # levels >= 3 are built by the matching launch itself (one workgroup per tile), unless
-        # the match schedule is per level
-        pyr.build(events=ev, wait=wait, nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream,
-                  defer_upper=self.schedule != L.DM_MATCH_PER_LEVEL)
+        pyr.build(events=ev, wait=wait, nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
         if diag:
             return torch.zeros((self.batch.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
-        return pyr.match(sub_pix=True, nlev=self.levels, schedule=self.schedule)
+        return pyr.match(sub_pix=True, nlev=self.levels)
 
     def level1_ms(self):
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
@@ -611,7 +602,7 @@ def c5_split(args, rank, world, dev, dist):
     del a, b
     voxels = grid * grid * float(tile) ** 4
     steps, warmup = args.c5_steps, 1
-    solver = PairSolver(img1, img2, tile, grid, split=world > 1, schedule=SCHEDULES[args.match_schedule])
+    solver = PairSolver(img1, img2, tile, grid, split=world > 1)
     pipe = Pipeline([solver], dev, dist, nstreams=max(1, args.streams), chain_levels=args.chain_levels)
     held = [] if not args.no_step_check else None
     el = pipe.run(steps, warmup, hold=held)
@@ -632,7 +623,7 @@ def c5_split(args, rank, world, dev, dist):
     ref_ms = ms
     if world > 1:
         if rank == 0:
-            alone = PairSolver(img1, img2, tile, grid, split=False, schedule=SCHEDULES[args.match_schedule])
+            alone = PairSolver(img1, img2, tile, grid, split=False)
             p1 = Pipeline([alone], dev, False, nstreams=max(1, args.streams), chain_levels=args.chain_levels)
             ref_ms = p1.run(steps, warmup) / steps * 1e3
             del p1, alone
@@ -686,8 +677,7 @@ def main():
     solvers = []
     for a, b in host_pairs:
         img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
-        solvers.append(PairSolver(img1, img2, tile, grid, split=split, levels=args.levels,
-                                  schedule=SCHEDULES[args.match_schedule]))
+        solvers.append(PairSolver(img1, img2, tile, grid, split=split, levels=args.levels))
     del host_pairs
     solver = solvers[0] if solvers else None
     voxels = grid * grid * float(tile) ** 4      # per pair
@@ -764,8 +754,7 @@ def main():
                           'pairs_per_gpu_per_step': per_gpu, 'parallelism': par,
                           'streams': nstreams, 'level_stream': bool(args.level_stream),
                           'stats_stream': bool(args.stats_stream and args.level_stream),
-                          'pair_priority': args.pair_priority, 'chain_levels': bool(args.chain_levels),
-                          'match_schedule': args.match_schedule},
+                          'pair_priority': args.pair_priority, 'chain_levels': bool(args.chain_levels)},
                'roofline': roof,
                'level_kernel_volume_equivalent': volume_equivalent(solver, tile, l1_ms)}
         if step_check is not None:

@@ -21,8 +21,6 @@ HEADER = os.path.join(os.path.dirname(HERE), 'include', 'dmstereo.h')
 DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3, -4
 DM_VOLUME_F16, DM_VOLUME_MINMAX_KNOWN = 1, 2   # dm_corr_volume_ex flags
 DM_POW_F32, DM_POW_Q4, DM_POW_K, DM_POW_FULL = 0, 1, 2, 3   # dm_pow14_variant forms
-DM_MATCH_AUTO, DM_MATCH_PER_LEVEL, DM_MATCH_PER_TILE = 0, 1, 2  # dm_match_ex schedules
-DM_MATCH_BUILD_UPPER = 4                                       # | per-tile: build levels 3.. too
 DM_TM_CCOEFF, DM_TM_CCOEFF_NORMED = 4, 5
 METHODS = {'cv2.TM_CCOEFF_NORMED': DM_TM_CCOEFF_NORMED, 'cv2.TM_CCOEFF': DM_TM_CCOEFF}
 CAL_MODES = {'elevation': 0, 'elevation2': 1, 'distance': 2}
@@ -65,8 +63,6 @@ SIGNATURES = {
     'dm_aggregate': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_match': ([_TP, _P, ctypes.POINTER(ctypes.c_void_p), _I, _I, _I, _I, _I, _I, _I, _I,
                   _P, _P, _P], ctypes.c_int),
-    'dm_match_ex': ([_TP, _P, ctypes.POINTER(ctypes.c_void_p), _I, _I, _I, _I, _I, _I, _I, _I, _I,
-                     _P, _P, _P], ctypes.c_int),
     'dm_sub_pix_cal': ([_P, _P, _I, _I, _I, ctypes.c_double, _P, _P], ctypes.c_int),
     'dm_cal_map': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_gs_schedule': ([_I, _I, _I, _I, _I, _I, _P, _P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),

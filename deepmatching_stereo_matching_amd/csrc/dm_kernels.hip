@@ -669,9 +669,8 @@ __device__ __forceinline__ void window_lvl(const double *M, int h, int w, int pd
 }
 
 // top of the pyramid (_initial_move_map, :80-96): p_dot = p, for entry p of tile t
-// Map buffers of the matching phases hold one (3, h, w) map per tile: tile t's at
-// map + t * ms, ms = 3 h w for the per-level launches (maps packed per level) and 3 h0 w0 for
-// k_tile_chain (a fixed region per tile: its tiles run different levels at once).
+// Map buffers of the matching phases hold one (3, h, w) map per tile: tile t's at map + t * ms
+// (ms = 3 h w: the maps of a level packed).
 __device__ __forceinline__ void match_top_at(const double *LK, int h, int w, size_t t, size_t p, double *map, size_t ms)
 {
     const size_t P = (size_t)h * w;
@@ -1362,66 +1361,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     subpix_at<WS>(g, s, (int)(idx / P), (int)(idx % P), map, 3 * P);
 }
 
-// ------------------------------------------------------------------------------------
-// The whole descent of dm_match for ONE tile per workgroup, in one launch: the top of the
-// pyramid, the _B steps on the stored levels K-1 .. 2, the steps onto level 1 and level 0 on
-// demand and the sub-pixel pass (Matching.py:80-209), each phase looping over the tile's
-// entries with the workgroup and separated by a workgroup barrier -- the same per-entry
-// device functions as the per-level kernels, so the maps are bit-identical.  A tile's
-// descent depends on that tile's pyramid only (image_cut_solver.py:115-142), so no other
-// synchronisation is needed.  Beside the next pair's level kernel this is one launch of T
-// workgroups that dispatch as soon as CUs free up, instead of ~10 dependent launches that
-// each wait for the level kernel's waves to drain.
-// Buffers alternate between b0 and b1 per phase; tile t's maps of every level live in its own
-// region t * 3 h0 w0 of them (its tiles run different levels at once, so the per-level
-// packing [T][3][h][w] of the per-level launches would let them overwrite each other), which
-// at level 0 is the packed [T][3][h0][w0] output.  The caller picks the buffers so that the
-// last phase lands in the output.
-#define TC_THREADS 512
-// build_from > 0: levels build_from + 1 .. K are first built from level build_from (the
-// pyramid's aggregation steps, Correlation_map.py:89-130 + :148, for this tile: aggregate_at,
-// k_aggregate's arithmetic) into lv's buffers -- the tile's levels depend on its own only.
-template <int WS>
-__global__ __launch_bounds__(TC_THREADS) void k_tile_chain(Geo g, Stats s, Levels lv, int nlev, int build_from,
-                                                        int sub_pix, double *b0, double *b1)
-{
-    DM_TAIL_ENTRY();
-    const int t = blockIdx.x, tid = threadIdx.x;
-    const int K = nlev - 1;
-    if (build_from > 0) {
-        for (int l = build_from + 1; l <= K; ++l) {
-            const int hp = g.h0 >> (l - 1), wp = g.w0 >> (l - 1);
-            const size_t n2 = (size_t)(hp / 2) * (wp / 2);
-            for (size_t i = tid; i < n2 * n2; i += TC_THREADS) aggregate_at(lv.lv[l - 1], hp, wp, 1, t, i, (double *)lv.lv[l]);
-            __syncthreads();
-        }
-    }
-    int h = g.h0 >> K, w = g.w0 >> K;
-    double *cur = b0, *nxt = b1;
-    const size_t ms = 3 * (size_t)g.h0 * g.w0;   // tile t's region in b0 / b1, every level
-    for (int p = tid; p < h * w; p += TC_THREADS) match_top_at(lv.lv[K], h, w, t, p, cur, ms);
-    for (int l = K - 1; l >= 0; --l) {
-        __syncthreads();
-        const int n = (2 * h) * (2 * w);
-        if (l == 0 && !lv.lv[0]) {
-            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_l0_at<WS>(g, s, t, pc, cur, ms, nxt, ms);
-        } else if (l == 1 && !lv.lv[1]) {
-            // four lanes (one quad) per entry: TC_THREADS % 4 == 0 and 4 n % 4 == 0, so a
-            // quad's lanes are live together
-            for (int i = tid; i < 4 * n; i += TC_THREADS)
-                match_step_l1_at<WS>(g, s, t, i >> 2, i & 3, true, cur, ms, nxt, ms);
-        } else {
-            for (int pc = tid; pc < n; pc += TC_THREADS) match_step_at(g, s, lv.lv[l], l, h, w, t, pc, cur, ms, nxt, ms);
-        }
-        double *x = cur; cur = nxt; nxt = x;
-        h *= 2; w *= 2;
-    }
-    if (sub_pix) {
-        __syncthreads();
-        for (int pc = tid; pc < h * w; pc += TC_THREADS) subpix_at<WS>(g, s, t, pc, cur, ms);
-    }
-}
-
 template <int WS>
 static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 {
@@ -1543,7 +1482,7 @@ static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, O
 
 extern "C" {
 
-int dm_abi_version(void) { return 108; }
+int dm_abi_version(void) { return 107; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1758,19 +1697,6 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
              int32_t T, int32_t h0, int32_t w0, int32_t sub_pix, int32_t filter_window,
              int32_t filter_num, int32_t filter_mode, double *d_scratch, double *d_out, void *stream)
 {
-    return dm_match_ex(b, d_stats, d_levels, nlev, T, h0, w0, sub_pix, filter_window, filter_num, filter_mode,
-                       DM_MATCH_AUTO, d_scratch, d_out, stream);
-}
-
-int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_levels, int32_t nlev,
-                int32_t T, int32_t h0, int32_t w0, int32_t sub_pix, int32_t filter_window,
-                int32_t filter_num, int32_t filter_mode, int32_t schedule, double *d_scratch, double *d_out,
-                void *stream)
-{
-    const int sched = schedule & 3;
-    const bool build_upper = (schedule & DM_MATCH_BUILD_UPPER) != 0;
-    if ((schedule & ~(3 | DM_MATCH_BUILD_UPPER)) || sched == 3 || (build_upper && sched == DM_MATCH_PER_LEVEL))
-        return fail(DM_ERR_ARG, "unknown matching schedule %d", schedule);
     if (!d_levels || !d_scratch || !d_out) return fail(DM_ERR_ARG, "null pointer");
     if (T < 1 || h0 < 1 || w0 < 1) return fail(DM_ERR_ARG, "empty batch (T=%d, h0=%d, w0=%d)", T, h0, w0);
     if (nlev < 2) return fail(DM_ERR_SHAPE, "list index out of range: Matching._B needs >= 2 levels (got %d)", nlev);
@@ -1795,25 +1721,8 @@ int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_l
         s = stats_view((void *)d_stats, T, h0 * w0);
     }
     hipStream_t st = (hipStream_t)stream;
-    // per-tile schedule: the whole descent in one launch of T workgroups (k_tile_chain), for
-    // level 0 on demand, no filter and ws = 5; AUTO takes it from 16 tiles up (below that a
-    // per-level launch spreads one tile's entries over more of the chip)
-    const bool tile_ok = !d_levels[0] && filter_num <= 0 && g.ws == 5;
-    if ((sched == DM_MATCH_PER_TILE || build_upper) && !tile_ok)
-        return fail(DM_ERR_UNSUPPORTED, "per-tile matching needs level 0 on demand, no filter and ws = 5");
-    if (build_upper && (nlev < 4 || !d_levels[2]))
-        return fail(DM_ERR_ARG, "DM_MATCH_BUILD_UPPER builds levels 3.. from a stored level 2 (nlev >= 4)");
-    if (tile_ok && (sched == DM_MATCH_PER_TILE || build_upper || (sched == DM_MATCH_AUTO && T >= 16))) {
-        Levels lv{};
-        for (int l = 0; l < nlev; ++l) lv.lv[l] = d_levels[l];
-        // K phases swap the buffers: start so that the last one writes d_out
-        double *b0 = (K & 1) ? d_scratch : d_out, *b1 = (K & 1) ? d_out : d_scratch;
-        k_tile_chain<5><<<T, TC_THREADS, 0, st>>>(g, s, lv, nlev, build_upper ? 2 : 0, sub_pix, b0, b1);
-        HIP_TRY(hipGetLastError());
-        return DM_OK;
-    }
-    // per-level schedule: one launch per phase; the buffer parity is chosen so that the last
-    // phase writes d_out (no copy): count the swaps (K steps + the filter passes that run)
+    // one launch per phase; the buffer parity is chosen so that the last phase writes d_out
+    // (no copy): count the swaps (K steps + the filter passes that run)
     int swaps = K;
     {
         int fl = filter_num, hh = h0 >> K, ww = w0 >> K;

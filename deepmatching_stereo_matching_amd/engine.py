@@ -122,7 +122,6 @@ class DevicePyramid:
             fuse_level2 = int(os.environ.get('DM_FUSE_L2', str(FUSE_DEFAULT)))
         self.fuse_level2 = int(fuse_level2)
         self.levels = [None]
-        self._pending_upper = False   # levels 3.. allocated by build(defer_upper=True), unbuilt
         self._volume = None
         self._have_minmax = False
         self._have_stats = False
@@ -180,7 +179,7 @@ class DevicePyramid:
         self._have_minmax = True
         return l1
 
-    def build(self, events=None, wait=None, nlev=None, level_stream=None, defer_upper=False):
+    def build(self, events=None, wait=None, nlev=None, level_stream=None):
         """Levels >= 1 up to level ``nlev`` - 1 (default: the full pyramid, as
         Correlation_map always builds it; a smaller ``nlev`` is the k-level pyramid of
         BASELINE configs C2/C3, whose levels above k - 1 Matching never reads).  ``events``:
@@ -193,11 +192,7 @@ class DevicePyramid:
         on (it waits for this pyramid's stats, and this pyramid's stream waits for it): a
         caller that sends every pair's level kernel to one such stream serialises them without
         events, and a pair's stats no longer queue behind the previous pair's tail on a shared
-        pair stream.  Building more levels later extends the pyramid.  ``defer_upper``: levels
-        3 .. nlev-1 are allocated but left for the next ``match()`` to build, in the same
-        per-tile launch as the descent (dm_match_ex DM_MATCH_BUILD_UPPER) -- where that applies
-        (level 2 fused and stored, level 0 on demand, ws = 5); any other read of them builds
-        them first with dm_aggregate."""
+        pair stream.  Building more levels later extends the pyramid."""
         b, lib = self.b, self.lib
         self.compute_stats()
         top = self.nlev if nlev is None else max(1, min(int(nlev), self.nlev))
@@ -250,13 +245,6 @@ class DevicePyramid:
                 done = torch.cuda.Event()
                 done.record(ls)
                 st.wait_event(done)
-        if (defer_upper and top >= 4 and len(self.levels) == 3 and self.levels[2] is not None
-                and b.ws == 5 and not self._pending_upper):
-            while len(self.levels) < top:                # allocated, built by match()
-                self.levels.append(self._empty_level(len(self.levels)))
-            self._pending_upper = True
-            return self
-        self._build_pending()
         while len(self.levels) < top:
             k = len(self.levels)               # build level k from level k - 1
             h, w = b.h0 >> (k - 1), b.w0 >> (k - 1)
@@ -265,18 +253,6 @@ class DevicePyramid:
                                      self._s()), 'dm_aggregate')
             self.levels.append(nxt)
         return self
-
-    def _build_pending(self):
-        """Levels 3.. left by build(defer_upper=True) and not yet built by match(): build
-        them now, with dm_aggregate, before anything reads them."""
-        if not self._pending_upper:
-            return
-        b = self.b
-        for k in range(3, len(self.levels)):
-            h, w = b.h0 >> (k - 1), b.w0 >> (k - 1)
-            L.check(self.lib.dm_aggregate(L.ptr(self.levels[k - 1]), b.T, h, w, 1, L.ptr(self.levels[k]),
-                                          self._s()), 'dm_aggregate')
-        self._pending_upper = False
 
     def level_shape(self, k):
         h, w = self.b.h0 >> k, self.b.w0 >> k
@@ -339,8 +315,6 @@ class DevicePyramid:
         if not 0 <= k < self.nlev:
             raise IndexError('list index out of range')
         if k > 0:
-            if k >= 3:
-                self._build_pending()
             if k >= len(self.levels):          # a k-level build: extend it
                 self.build(nlev=k + 1)
             if self.levels[k] is None:   # level 1 kept on chip by dm_corr_level12
@@ -352,15 +326,13 @@ class DevicePyramid:
         return out
 
     def match(self, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
-              filtering_mode='median', levels=None, nlev=None, schedule=L.DM_MATCH_AUTO):
+              filtering_mode='median', levels=None, nlev=None):
         """Matching()() for every tile: float64 [T][3][h0][w0] (row, col, score).
         ``levels``: an explicit co_map_list (e.g. materialized_levels()) to match on
         instead of this pyramid's (level 0 then read from memory, not re-derived).
         ``nlev``: match on the first ``nlev`` levels only, the reference's Matching on a
         co_map_list cut to k levels with N_map = 2^(k-1): the descent
-        starts at level nlev - 1, one start per cell of that level (Matching.py:80-96).
-        ``schedule``: dm_match_ex's launch schedule (one launch per phase, or the whole
-        descent in one launch with a workgroup per tile); the results are the same."""
+        starts at level nlev - 1, one start per cell of that level (Matching.py:80-96)."""
         b = self.b
         n = self.nlev if nlev is None else int(nlev)
         if not 1 <= n <= self.nlev:
@@ -380,18 +352,10 @@ class DevicePyramid:
             ptrs = (ctypes.c_void_p * n)(*([None] + [None if t is None else t.data_ptr()
                                                       for t in self.levels[1:n]]))
         fnum = int(filtering_num) if filtering else 0
-        sched = int(schedule)
-        if self._pending_upper:
-            if (levels is None and n == len(self.levels) and fnum == 0 and
-                    sched != L.DM_MATCH_PER_LEVEL):
-                sched |= L.DM_MATCH_BUILD_UPPER       # build levels 3.. in the same launch
-                self._pending_upper = False
-            else:
-                self._build_pending()
-        L.check(self.lib.dm_match_ex(b.ref(), L.ptr(self.stats), ptrs, n, b.T, b.h0, b.w0,
-                                     int(bool(sub_pix)), int(filter_window_size), fnum,
-                                     1 if filtering_mode == 'median' else 0, sched,
-                                     L.ptr(scratch), L.ptr(out), self._s()), 'dm_match_ex')
+        L.check(self.lib.dm_match(b.ref(), L.ptr(self.stats), ptrs, n, b.T, b.h0, b.w0,
+                                  int(bool(sub_pix)), int(filter_window_size), fnum,
+                                  1 if filtering_mode == 'median' else 0,
+                                  L.ptr(scratch), L.ptr(out), self._s()), 'dm_match')
         return out
 
 

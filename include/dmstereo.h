@@ -172,24 +172,6 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
              int32_t filter_window, int32_t filter_num, int32_t filter_mode,
              double *d_scratch, double *d_out, void *stream);
 
-/* dm_match with an explicit launch schedule (same results bit for bit, ABI 1.8):
- *   DM_MATCH_PER_LEVEL  one launch per phase (top, each _B step, sub-pixel), every tile's
- *                       entries spread over the chip;
- *   DM_MATCH_PER_TILE   the whole descent in ONE launch, one workgroup per tile (level 0 on
- *                       demand, no filter, ws = 5; DM_ERR_UNSUPPORTED otherwise): a pipelined
- *                       caller's tail is then one launch that runs beside the next pair's level
- *                       kernel instead of ~10 dependent ones waiting for it to drain;
- *   DM_MATCH_AUTO       PER_TILE where it applies and T >= 16, else PER_LEVEL (= dm_match).
- * | DM_MATCH_BUILD_UPPER (per-tile only): d_levels[3 .. nlev-1] are OUTPUT buffers, built in
- *   the same launch from the stored level 2 (dm_aggregate's arithmetic, rectify on) before
- *   the descent -- the pyramid's last aggregation steps join the one-launch tail. */
-enum dm_match_schedule { DM_MATCH_AUTO = 0, DM_MATCH_PER_LEVEL = 1, DM_MATCH_PER_TILE = 2,
-                         DM_MATCH_BUILD_UPPER = 4 };
-int dm_match_ex(const dm_tiles *b, const void *d_stats, const double *const *d_levels,
-                int32_t nlev, int32_t T, int32_t h0, int32_t w0, int32_t sub_pix,
-                int32_t filter_window, int32_t filter_num, int32_t filter_mode, int32_t schedule,
-                double *d_scratch, double *d_out, void *stream);
-
 /* misc/sub_pix_cal.py sub_pix_cal (:22-53): clamp to [-3,3], quadratic refinement of an
  * (h, w) disparity map along `direction` (0 rows, 1 cols) on the score map scaled by
  * `ratio`, reject |delta| > 1, clamp again.  float64 in/out, device pointers. */
@@ -277,12 +259,11 @@ int dm_seq_sum(const double *d_v, int64_t n, double *d_out, void *stream);
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 108 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 107 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
  * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
- * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum,
- * 1.8 dm_match_ex). */
+ * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

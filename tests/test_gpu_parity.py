@@ -565,79 +565,3 @@ def test_matching_sweep_vs_oracle(h0, w0, ws, method, seed, mirror):
     if len(olev) > 1:
         _same(MT.Matching(co)(), O.match(olev, sub_pix=True))
 
-
-@pytest.mark.parametrize('S,T,ws', [(32, 20, 5), (64, 17, 5), (128, 16, 5), (16, 18, 5)])
-def test_match_schedules_identical(S, T, ws):
-    """dm_match_ex's two launch schedules -- one launch per phase, and the whole descent in ONE
-    launch with a workgroup per tile (k_tile_chain) -- give the same maps bit for bit: full and
-    k-level pyramids, with and without sub-pixel, constant patches (NaN maps) included; and
-    AUTO (= dm_match) is the per-tile one from 16 tiles up.  (tests/test_c3_batch.py pins the
-    AUTO path of the bench's 64-tile batches to the oracle tile by tile.)"""
-    from deepmatching_stereo_matching_amd import _lib as L
-    from deepmatching_stereo_matching_amd import engine
-    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
-    side = S + ws - 1
-    a, b = stereo_pair(side + 3 * T, side + 5, seed=S + T, dx=2, sinusoidal=True)
-    a[5:5 + ws + 2, 4:4 + ws] = 60                      # flat patches in the first tiles
-    org = [(3 * t, (t * 7) % 6) for t in range(T)]
-    pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, ws, 5))
-    for sub_pix in (True, False):
-        for nlev in sorted({pyr.nlev, 3}):
-            lvl = pyr.match(sub_pix=sub_pix, nlev=nlev, schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy()
-            til = pyr.match(sub_pix=sub_pix, nlev=nlev, schedule=L.DM_MATCH_PER_TILE).cpu().numpy()
-            auto = pyr.match(sub_pix=sub_pix, nlev=nlev).cpu().numpy()
-            _same(til, lvl)
-            _same(auto, lvl)
-    if S <= 32:   # and against the oracle, tile by tile
-        for t, (r, c) in enumerate(org[:4]):
-            lv, _, _ = O.pyramid(O.corr_l0(a[r:r + side, c:c + side], b[r:r + side, c:c + side], ws))
-            _same(pyr.match(schedule=L.DM_MATCH_PER_TILE).cpu().numpy()[t], O.match(lv, sub_pix=True))
-
-
-def test_match_per_tile_unsupported_cases():
-    from deepmatching_stereo_matching_amd import _lib as L
-    from deepmatching_stereo_matching_amd import engine
-    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
-    a, b = stereo_pair(40, 40, seed=9, dx=2)
-    pyr = engine.DevicePyramid(engine.TileBatch(a, b, [(0, 0), (2, 2)], 32, 32, 5, 5))
-    with pytest.raises(Exception, match='per-tile'):
-        pyr.match(filtering=True, schedule=L.DM_MATCH_PER_TILE)
-    a3, b3 = stereo_pair(36, 36, seed=9, dx=2)
-    p3 = engine.DevicePyramid(engine.TileBatch(a3, b3, [(0, 0)], 32, 32, 3, 5))
-    with pytest.raises(Exception, match='per-tile'):
-        p3.match(schedule=L.DM_MATCH_PER_TILE)
-    with pytest.raises(Exception, match='schedule'):
-        p3.match(schedule=7)
-    # the per-level schedule still takes both
-    _same(p3.match(schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy(), p3.match().cpu().numpy())
-
-
-@pytest.mark.parametrize('S,T,nlev', [(32, 18, None), (64, 16, None), (64, 16, 4), (128, 16, 5)])
-def test_match_builds_upper_levels(S, T, nlev):
-    """build(defer_upper=True) + match(): levels 3.. are built inside the per-tile matching
-    launch (DM_MATCH_BUILD_UPPER); levels, maps and sub-pixel equal the eager dm_aggregate
-    build + per-level matching bit for bit, and a later read of a deferred level is correct."""
-    from deepmatching_stereo_matching_amd import _lib as L
-    from deepmatching_stereo_matching_amd import engine
-    from deepmatching_stereo_matching_amd.synthetic import stereo_pair
-    side = S + 4
-    a, b = stereo_pair(side + 2 * T, side + 3, seed=3 * S + T, dx=2, sinusoidal=True)
-    a[7:7 + 6, 9:9 + 5] = 200
-    org = [(2 * t, t % 4) for t in range(T)]
-    ref = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
-    ref.build(nlev=nlev)
-    want = ref.match(nlev=nlev, schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy()
-    top = ref.nlev if nlev is None else nlev
-    pyr = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
-    pyr.build(nlev=nlev, defer_upper=True)
-    assert pyr._pending_upper == (top >= 4)
-    _same(pyr.match(nlev=nlev).cpu().numpy(), want)
-    assert not pyr._pending_upper
-    for k in range(3, top):
-        _same(pyr.levels[k].cpu().numpy(), ref.levels[k].cpu().numpy())
-    # a deferred level read before any match is built on demand
-    lazy = engine.DevicePyramid(engine.TileBatch(a, b, org, S, S, 5, 5), build=False)
-    lazy.build(nlev=nlev, defer_upper=True)
-    if top >= 4:
-        _same(lazy.level(top - 1).cpu().numpy(), ref.levels[top - 1].cpu().numpy())
-        _same(lazy.match(nlev=nlev, schedule=L.DM_MATCH_PER_LEVEL).cpu().numpy(), want)

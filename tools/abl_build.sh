@@ -3,6 +3,8 @@
 #   nobar   no barrier between the two waves of a workgroup in sweep 2 (dm_mfma.h:628)
 #   nopow   pow14_zf replaced by a widening multiply (the eight child pows per row pair)
 #   nosw1   sweep 1 (per-patch min / max) skipped
+#   pconst  pow14_zf's three LDS table reads at fixed rows (broadcast: no bank conflicts)
+#   pnoread pow14_zf without its LDS table reads (values from the index bits, no LDS)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -22,6 +24,22 @@ open(p, 'w').write(s)
 PY
     ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
+    pconst) sed -i 's/    const unsigned ofp = (u >> 10) \& 0x1FF0u, og = (u >> 19) \& 0xFF0u;/    const unsigned ofp = (u \& 0u), og = (u \& 0u) + 16u;/' $d/csrc/dm_kernels.hip
+            grep -q "ofp = (u & 0u)" $d/csrc/dm_kernels.hip || { echo "pconst patch failed"; exit 1; } ;;
+    pnoread) python3 - $d/csrc/dm_kernels.hip <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """    const float ci = *(const float *)((const char *)t.fc32 + (ofp >> 2));
+    const dm_d2 G = *(const dm_d2 *)((const char *)t.g32 + og);
+    const dm_d2 Pr = *(const dm_d2 *)((const char *)t.fp + ofp);"""
+new = """    const float ci = __uint_as_float(0x3F800000u | (ofp & 0x70u));
+    const dm_d2 G = dm_d2{1.0 + (double)(og & 0x30u), 1e-17};
+    const dm_d2 Pr = dm_d2{1.0 + (double)(ofp & 0x30u), 1e-17};"""
+assert s.count(old) == 1
+s = s.replace(old, new)
+open(p, 'w').write(s)
+PY
+    ;;
     base) ;;
     *) echo "unknown $v"; exit 2 ;;
   esac

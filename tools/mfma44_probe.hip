@@ -120,11 +120,14 @@ int main()
     long long *dc, hc[1024];
     v4i *sink;
     float *fs;
-    hipMalloc(&dc, 8 * 1024); hipMalloc(&sink, 1024 * 64 * 16); hipMalloc(&fs, 4096);
+    // sized for the largest grid below: 4096 one-wave blocks
+    hipMalloc(&dc, 8 * 4096); hipMalloc(&sink, (size_t)4096 * 64 * 16); hipMalloc(&fs, 4096);
     hipMemset(fs, 0, 4096);
     auto run = [&](const char *name, auto kern, int waves_per_simd) {
         const int blocks = 256 * 4 * waves_per_simd;   // one-wave blocks spread over 1024 SIMDs
+        if (blocks > 4096) { printf("grid too large\n"); return; }
         kern<<<blocks, 64>>>(3, 5, dc, sink, fs);       // warm
+        if (hipDeviceSynchronize() != hipSuccess) { printf("%s: launch failed\n", name); return; }
         hipEvent_t e0, e1;
         hipEventCreate(&e0); hipEventCreate(&e1);
         hipEventRecord(e0);
