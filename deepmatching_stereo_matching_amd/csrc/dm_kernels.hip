@@ -1435,6 +1435,9 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 
 // LDS-shared-window volume kernel (k_volume_ls): ws <= 5 on the MFMA shapes, 8 waves (patch
 // blocks) per workgroup, nontemporal stores
+#ifndef DM_VOLUME_TR
+#define DM_VOLUME_TR 0
+#endif
 template <typename OT>
 static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st,
                             int have_mm = 0)
@@ -1454,7 +1457,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
-#define DM_VL(G_) if (G == G_) { k_volume_ls<G_, 8, true, OT><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
+#define DM_VL(G_) if (G == G_) { constexpr bool TR_ = DM_VOLUME_TR && (int)(16 / sizeof(OT)) <= G_; k_volume_ls<G_, 8, true, OT, TR_><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_VL(2) DM_VL(4) DM_VL(8) DM_VL(16)
 #undef DM_VL
     return DM_ERR_UNSUPPORTED;

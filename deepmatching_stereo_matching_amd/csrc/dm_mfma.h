@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // run per store instruction, no LDS stage.
 // Arithmetic per voxel is k_volume_mfq's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
-template <int G, int NW, bool NT, typename OT, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
+template <int G, int NW, bool NT, typename OT, bool TR = false, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                    const int2 *__restrict__ QS, OT *vol, int have_mm)
 {
@@ -1053,6 +1053,86 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
     // constant patches need it)
     auto sweep2 = [&](auto clamp_tag) {
     constexpr bool CL = decltype(clamp_tag)::value;
+    // x of tile tau's window column c for this lane's 4 patches, into element tw of v[0..3]
+    auto x_tile = [&](int buf, int tau, ov *v, int tw) {
+        float y[4];
+        tile_y(buf, tau, y);
+        const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
+        const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
+        dm_f2 r01 = ya, r23 = yb;
+        if constexpr (CL) {
+            r01 = dm_f2{__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1])};
+            r23 = dm_f2{__builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
+        }
+        const dm_f2 a01 = r01 - dm_f2{rmn[0], rmn[1]};
+        const dm_f2 a23 = r23 - dm_f2{rmn[2], rmn[3]};
+        const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
+        const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
+        const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
+        const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
+        const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
+        const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
+        v[0][tw] = (OT)x01.x; v[1][tw] = (OT)x01.y; v[2][tw] = (OT)x23.x; v[3][tw] = (OT)x23.y;
+    };
+    if constexpr (TR) {
+        // 1-KB stores: RB rows of NCG 256-B column groups are four consecutive 256-B chunks of
+        // each patch map.  Lane group g computed chunk i of its own patches (g, r); a 4 x 4
+        // transpose over the lane groups (permlane32 then permlane16 swaps, per dword) leaves
+        // lane group g with chunk g of patch (s, r) in X[r][s], so one store instruction writes
+        // 1 KB of ONE map (the maps' rows are consecutive) instead of 256 B of four.
+        constexpr int NCG = G / CH, RB = 4 / NCG;
+        static_assert(CH * sizeof(OT) == 16 && NCG <= 4 && 4 % NCG == 0, "1-KB bursts need 16-B lanes");
+        OT *const pb = vol + (tb + (size_t)(2 * I0) * W0 + 2 * J0) * (size_t)P;   // patch (0, 0)
+        const int loff = grp * 16 * CH + GW * c;
+        for (int q0 = 0; q0 < h0; q0 += RB) {
+            dm_v4i X[4][4];   // [r][i]: chunk i = k NCG + j of the burst, patch (grp, r)
+#pragma unroll
+            for (int k = 0; k < RB; ++k) {
+                const int q = q0 + k;
+                const int buf = (h0 + q) & 1;
+                if (q + 1 < h0) fill(q + 1, buf ^ 1);
+#pragma unroll
+                for (int j = 0; j < NCG; ++j) {
+                    ov v[4];
+#pragma unroll
+                    for (int tw = 0; tw < CH; ++tw) x_tile(buf, j * CH + tw, v, tw);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) X[r][k * NCG + j] = __builtin_bit_cast(dm_v4i, v[r]);
+                }
+                if (k + 1 < RB) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) {   // halves: groups 2, 3 of chunk a <-> groups 0, 1 of chunk a + 2
+                        const auto w = __builtin_amdgcn_permlane32_swap(X[r][a][d], X[r][a + 2][d], false, false);
+                        X[r][a][d] = (int)w[0];
+                        X[r][a + 2][d] = (int)w[1];
+                    }
+#pragma unroll
+                    for (int a = 0; a < 4; a += 2) { // odd rows of 16 lanes of a <-> even rows of a + 1
+                        const auto w = __builtin_amdgcn_permlane16_swap(X[r][a][d], X[r][a + 1][d], false, false);
+                        X[r][a][d] = (int)w[0];
+                        X[r][a + 1][d] = (int)w[1];
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const size_t pofs = (size_t)((2 * (s2 >> 1) + (r >> 1)) * W0 + 2 * (s2 & 1) + (r & 1)) * (size_t)P;
+                    ov *dst = (ov *)(pb + pofs + (size_t)q0 * W0 + loff);
+                    const ov o = __builtin_bit_cast(ov, X[r][s2]);
+                    if constexpr (NT) __builtin_nontemporal_store(o, dst);
+                    else *dst = o;
+                }
+            }
+            if (q0 + RB < h0) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        }
+    } else {
     for (int q0 = 0; q0 < h0; ++q0) {
         const int buf = (h0 + q0) & 1;
         if (q0 + 1 < h0) fill(q0 + 1, buf ^ 1);
@@ -1060,26 +1140,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         for (int t0 = 0; t0 < G; t0 += CH) {
             ov v[4];
 #pragma unroll
-            for (int tw = 0; tw < CH; ++tw) {
-                float y[4];
-                tile_y(buf, t0 + tw, y);
-                const dm_f2 ya = dm_f2{y[0], y[1]} * dm_f2{ap[0], ap[1]};
-                const dm_f2 yb = dm_f2{y[2], y[3]} * dm_f2{ap[2], ap[3]};
-                dm_f2 r01 = ya, r23 = yb;
-                if constexpr (CL) {
-                    r01 = dm_f2{__builtin_amdgcn_fmed3f(ya.x, lo[0], hi[0]), __builtin_amdgcn_fmed3f(ya.y, lo[1], hi[1])};
-                    r23 = dm_f2{__builtin_amdgcn_fmed3f(yb.x, lo[2], hi[2]), __builtin_amdgcn_fmed3f(yb.y, lo[3], hi[3])};
-                }
-                const dm_f2 a01 = r01 - dm_f2{rmn[0], rmn[1]};
-                const dm_f2 a23 = r23 - dm_f2{rmn[2], rmn[3]};
-                const dm_f2 i01 = {rinv[0], rinv[1]}, i23 = {rinv[2], rinv[3]};
-                const dm_f2 q01 = a01 * i01, q23 = a23 * i23;
-                const dm_f2 e01 = __builtin_elementwise_fma(-q01, dm_f2{den[0], den[1]}, a01);
-                const dm_f2 e23 = __builtin_elementwise_fma(-q23, dm_f2{den[2], den[3]}, a23);
-                const dm_f2 x01 = __builtin_elementwise_fma(e01, i01, q01);
-                const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
-                v[0][tw] = (OT)x01.x; v[1][tw] = (OT)x01.y; v[2][tw] = (OT)x23.x; v[3][tw] = (OT)x23.y;
-            }
+            for (int tw = 0; tw < CH; ++tw) x_tile(buf, t0 + tw, v, tw);
             const int col = q0 * W0 + 16 * t0;    // column group t0 / GW starts at window 16 GW (t0 / GW)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1094,6 +1155,7 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
             else if constexpr (STORES == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
+    }
     }
     };
     if (clamp) sweep2(std::true_type{});

@@ -5,6 +5,9 @@
 #   nosw1   sweep 1 (per-patch min / max) skipped
 #   pconst  pow14_zf's three LDS table reads at fixed rows (broadcast: no bank conflicts)
 #   pnoread pow14_zf without its LDS table reads (values from the index bits, no LDS)
+#   prow    c_i and a float32 (1/c_i)^y lo packed into the fp row: one b128 read instead of
+#           b128 + b32 (a layout probe: the row's contents are not rebuilt)
+#   vtr     k_volume_ls with its 1-KB transposed stores (DM_VOLUME_TR 1; results exact)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -40,6 +43,24 @@ s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
     ;;
+    prow) python3 - $d/csrc/dm_kernels.hip <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """    const float ci = *(const float *)((const char *)t.fc32 + (ofp >> 2));
+    const dm_d2 G = *(const dm_d2 *)((const char *)t.g32 + og);
+    const dm_d2 Pr = *(const dm_d2 *)((const char *)t.fp + ofp);"""
+new = """    const dm_d2 G = *(const dm_d2 *)((const char *)t.g32 + og);
+    const dm_d2 P0 = *(const dm_d2 *)((const char *)t.fp + ofp);
+    const unsigned long long lo_ = (unsigned long long)__double_as_longlong(P0.y);
+    const float ci = __uint_as_float((unsigned)lo_);
+    const dm_d2 Pr = dm_d2{P0.x, (double)__uint_as_float((unsigned)(lo_ >> 32))};"""
+assert s.count(old) == 1
+s = s.replace(old, new)
+open(p, 'w').write(s)
+PY
+    ;;
+    vtr) sed -i 's/^#define DM_VOLUME_TR 0$/#define DM_VOLUME_TR 1/' $d/csrc/dm_kernels.hip
+         grep -q '^#define DM_VOLUME_TR 1$' $d/csrc/dm_kernels.hip || { echo "vtr patch failed"; exit 1; } ;;
     base) ;;
     *) echo "unknown $v"; exit 2 ;;
   esac

@@ -23,8 +23,8 @@ EM_AMDGPU = 224
 LEVEL = {64: 'k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi2ELb1EE',      # C2: NB = 2 blocks per workgroup
          128: 'k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi1ELb1EE',     # C3: GW = 4, 2 waves
          256: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}     # C5: GW = 4, 4 waves
-VOLUME = {(128, 4): 'k_volume_lsILi8ELi8ELb1EfLi', (128, 2): 'k_volume_lsILi8ELi8ELb1EDF16_',
-          (256, 4): 'k_volume_lsILi16ELi8ELb1EfLi', (256, 2): 'k_volume_lsILi16ELi8ELb1EDF16_'}
+VOLUME = {(128, 4): 'k_volume_lsILi8ELi8ELb1EfL', (128, 2): 'k_volume_lsILi8ELi8ELb1EDF16_L',
+          (256, 4): 'k_volume_lsILi16ELi8ELb1EfL', (256, 2): 'k_volume_lsILi16ELi8ELb1EDF16_L'}
 
 
 def symbol(kind, tile, esz=None):

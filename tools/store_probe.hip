@@ -6,6 +6,9 @@
 //           per image row and accumulator row, S*esz/256 stores of 4 x 256 B into 4 patch maps,
 //           the maps advancing S*esz bytes per row (rows of one map are consecutive)
 //   vol4  : four image rows per burst
+//   volx  : k_volume_ls's patches and order, but each store instruction 1 KB of ONE patch map
+//           (lane group g writes the map's 256-B chunk 4k + g): the pattern a cross-lane-group
+//           transpose of four rows' results would give
 // each with plain or nontemporal stores, 8 waves per workgroup as k_volume_ls.  No arithmetic:
 // the rate each pattern allows the write path.  One JSON line per shape on stdout.
 //   hipcc -O3 --offload-arch=gfx950 tools/store_probe.hip -o tools/store_probe.bin
@@ -60,6 +63,28 @@ __global__ __launch_bounds__(512) void k_vol(char *vol, int S, int esz)
         for (int r = 0; r < 4; ++r)
             for (int k = 0; k < RB; ++k)
                 for (int j = 0; j < per_row; ++j) st16<NT>(out[r] + (size_t)(q0 + k) * rowb + j * 256, v);
+    }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(512) void k_volx(char *vol, int S, int esz)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = lane & 15, grp = lane >> 4;
+    const size_t P = (size_t)S * S, mapb = P * esz;
+    const size_t blk = (size_t)blockIdx.x * 8 + wave;
+    const size_t bpt = (size_t)(S / 4) * (S / 4);
+    const size_t t = blk / bpt, bi = blk % bpt;
+    const int I0 = 2 * (int)(bi / (S / 4)), J0 = 2 * (int)(bi % (S / 4));
+    const v4u v = {(unsigned)lane, 1u, 2u, 3u};
+    const int chunks = (int)(mapb / 256);
+    for (int q = 0; q < chunks; q += 4) {
+#pragma unroll
+        for (int pp = 0; pp < 16; ++pp) {
+            const int g = pp >> 2, r = pp & 3;
+            const size_t p = (size_t)(2 * (I0 + (g >> 1)) + (r >> 1)) * S + 2 * (J0 + (g & 1)) + (r & 1);
+            st16<NT>(vol + (t * P + p) * mapb + (size_t)(q + grp) * 256 + c * 16, v);
+        }
     }
 }
 
@@ -124,6 +149,8 @@ int main(int argc, char **argv)
         run("vol_rot", [&] { k_vol<1, false, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("vol4", [&] { k_vol<4, false><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("vol4_nt", [&] { k_vol<4, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("volx", [&] { k_volx<false><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("volx_nt", [&] { k_volx<true><<<grid, 512>>>(vol, sh.S, sh.esz); });
         printf("}\n");
         fflush(stdout);
     }
