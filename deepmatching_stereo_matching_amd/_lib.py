@@ -63,6 +63,7 @@ SIGNATURES = {
     'dm_aggregate': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_match': ([_TP, _P, ctypes.POINTER(ctypes.c_void_p), _I, _I, _I, _I, _I, _I, _I, _I,
                   _P, _P, _P], ctypes.c_int),
+    'dm_subpix_map': ([_P, _I, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_sub_pix_cal': ([_P, _P, _I, _I, _I, ctypes.c_double, _P, _P], ctypes.c_int),
     'dm_cal_map': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_gs_schedule': ([_I, _I, _I, _I, _I, _I, _P, _P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),

@@ -987,21 +987,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
     match_step_l1_at<WS>(g, s, (int)(ee / P1), (int)(ee % P1), (int)(gid & 3), live, pmap, 3 * (P1 / 4), cmap, 3 * P1);
 }
 
-// Matching._sub_pix_cal (:177-209) on the final level-0 map, in place.  L0: materialised
-// rectified level 0 ([T][P][P]) or nullptr (on demand from images + stats).
-__global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, double *map)
+// Matching._sub_pix_cal (:177-209) on the final map, in place.  L0: materialised rectified
+// level 0 ([T][P0][P0], P0 = h0 w0) or nullptr (on demand from images + stats).  The map is
+// hm x wm: h0 x w0 after a descent to level 0, a coarser level's when the descent stops
+// above it -- the reference still reads co_map_list[0] at (i, j, row, col) of that map
+// (:182-186), so the level-0 patch is (i, j) and the bounds are level 0's window sides.
+// Indices outside [0, h0) x [0, w0) leave the entry as it is (the reference's IndexError
+// branch; a matching descent never produces them).
+__global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, int hm, int wm, double *map)
 {
     DM_TAIL_ENTRY();
-    const size_t P = (size_t)h0 * w0;
+    const size_t P = (size_t)h0 * w0, Pm = (size_t)hm * wm;
     const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (idx >= (size_t)T * P) return;
-    const int t = (int)(idx / P), pc = (int)(idx % P);
-    const int p0 = pc / w0, p1 = pc % w0;
-    double *mt = map + (size_t)t * 3 * P;
-    const double *M = L0 ? L0 + ((size_t)t * P + pc) * P : nullptr;
+    if (idx >= (size_t)T * Pm) return;
+    const int t = (int)(idx / Pm), pc = (int)(idx % Pm);
+    const int p0 = pc / wm, p1 = pc % wm;
+    double *mt = map + (size_t)t * 3 * Pm;
+    const double *M = L0 ? L0 + ((size_t)t * P + (size_t)p0 * w0 + p1) * P : nullptr;
 #define L0V(r_, c_) (M ? M[(size_t)(r_) * w0 + (c_)] : l0_value(g, s, t, p0, p1, (r_), (c_)))
-    const double row = mt[pc], col = mt[P + pc];
+    const double row = mt[pc], col = mt[Pm + pc];
     const int c0 = (int)row, c1 = (int)col; // int() truncation of exact integers
+    if (!(c0 >= 0 && c0 < h0 && c1 >= 0 && c1 < w0)) return;
     const double r0 = L0V(c0, c1);
     const double dx = (double)p0 - row;
     double nrow, ncol;
@@ -1020,7 +1026,7 @@ __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0
     }
 #undef L0V
     mt[pc] = nrow;
-    mt[P + pc] = ncol;
+    mt[Pm + pc] = ncol;
 }
 
 // Matching._filter (:224-255), square maps: per interior pixel the rounded (half-even)
@@ -1377,6 +1383,9 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
+#ifndef DM_C2_NB
+#define DM_C2_NB 4   // one-wave cell blocks per workgroup of the S = 64 level kernel
+#endif
 template <bool L2F, bool YF>
 static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
                         hipStream_t st)
@@ -1393,12 +1402,15 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
-    // GW = 4 with one wave per cell block (S = 64, C2): two cell blocks per workgroup share
-    // the pow tables (one-wave workgroups would hold 20 KB of LDS per wave: 2 waves/SIMD)
+    // GW = 4 with one wave per cell block (S = 64, C2): C2_NB cell blocks per workgroup share
+    // the pow tables (one-wave workgroups would hold 20 KB of LDS per wave: 2 waves/SIMD).
+    // 4 blocks: C2 level kernel 0.540 -> 0.503-0.509 ms against 2 (same box,
+    // profiles/r04g_c2nb4.txt): half the table fills and workgroup starts per wave
     if (KS == 1 && GW == 4 && NW == 1) {
+        constexpr int NBc = DM_C2_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
-        if (((size_t)b->T * bpt) % 2) return fail(DM_ERR_UNSUPPORTED, "odd cell-block count");
-        k_level1_mfq<1, 4, 2, 4, L2F, YF, 2, CL><<<grid / 2, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1435,8 +1447,24 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 
 // LDS-shared-window volume kernel (k_volume_ls): ws <= 5 on the MFMA shapes, 8 waves (patch
 // blocks) per workgroup, nontemporal stores
-#ifndef DM_VOLUME_TR
-#define DM_VOLUME_TR 0
+// The w0 = 128 (C3) instances: store runs (TR), register budget (waves per SIMD, MW) and
+// nontemporal stores (NT) per output type, chosen by same-box A/B.
+// binary16 with the min/max known (no min/max sweep):
+#ifndef DM_VL_H_TR
+#define DM_VL_H_TR 0
+#endif
+#ifndef DM_VL_H_NT
+#define DM_VL_H_NT 1
+#endif
+// float32:
+#ifndef DM_VL_F_TR
+#define DM_VL_F_TR 0
+#endif
+#ifndef DM_VL_F_MW
+#define DM_VL_F_MW 1
+#endif
+#ifndef DM_VL_F_NT
+#define DM_VL_F_NT 1
 #endif
 template <typename OT>
 static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st,
@@ -1457,7 +1485,20 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(b->T * bpt / nw);
     const Geo gg = make_geo(b);
-#define DM_VL(G_) if (G == G_) { constexpr bool TR_ = DM_VOLUME_TR && (int)(16 / sizeof(OT)) <= G_; k_volume_ls<G_, 8, true, OT, TR_><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
+    if (G == 8) {
+        if constexpr (sizeof(OT) == 2) {
+            if (have_mm) {
+                k_volume_ls<8, 8, DM_VL_H_NT, OT, DM_VL_H_TR><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+                HIP_TRY(hipGetLastError());
+                return DM_OK;
+            }
+        } else {
+            k_volume_ls<8, 8, DM_VL_F_NT, OT, DM_VL_F_TR, DM_VL_F_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+    }
+#define DM_VL(G_) if (G == G_) { k_volume_ls<G_, 8, true, OT><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_VL(2) DM_VL(4) DM_VL(8) DM_VL(16)
 #undef DM_VL
     return DM_ERR_UNSUPPORTED;
@@ -1485,7 +1526,7 @@ static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, O
 
 extern "C" {
 
-int dm_abi_version(void) { return 107; }
+int dm_abi_version(void) { return 108; }
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1808,12 +1849,25 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
             default: k_subpix_t<15><<<nb, 256, 0, st>>>(g, s, T, buf[cur]); break;
             }
         } else {
-            k_subpix<<<nblk((size_t)T * h0 * w0, 64), 64, 0, st>>>(g, s, d_levels[0], T, h0, w0, buf[cur]);
+            k_subpix<<<nblk((size_t)T * h0 * w0, 64), 64, 0, st>>>(g, s, d_levels[0], T, h0, w0, h0, w0, buf[cur]);
         }
         HIP_TRY(hipGetLastError());
     }
     if (buf[cur] != d_out) // (the parity above makes this unreachable; kept as a guard)
         HIP_TRY(hipMemcpyAsync(d_out, buf[cur], sizeof(double) * 3 * (size_t)T * h0 * w0, hipMemcpyDeviceToDevice, st));
+    return DM_OK;
+}
+
+int dm_subpix_map(const double *d_level0, int32_t T, int32_t h0, int32_t w0, int32_t hm, int32_t wm,
+                  double *d_map, void *stream)
+{
+    if (!d_level0 || !d_map) return fail(DM_ERR_ARG, "dm_subpix_map needs level 0 and the map");
+    if (T < 1 || h0 < 1 || w0 < 1 || hm < 1 || wm < 1 || hm > h0 || wm > w0)
+        return fail(DM_ERR_ARG, "dm_subpix_map: T=%d level 0 %dx%d map %dx%d", T, h0, w0, hm, wm);
+    const Geo g{};
+    const Stats s{};
+    k_subpix<<<nblk((size_t)T * hm * wm, 64), 64, 0, (hipStream_t)stream>>>(g, s, d_level0, T, h0, w0, hm, wm, d_map);
+    HIP_TRY(hipGetLastError());
     return DM_OK;
 }
 

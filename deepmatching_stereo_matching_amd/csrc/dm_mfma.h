@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // run per store instruction, no LDS stage.
 // Arithmetic per voxel is k_volume_mfq's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
-template <int G, int NW, bool NT, typename OT, bool TR = false, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
+template <int G, int NW, bool NT, typename OT, int TR = 0, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                    const int2 *__restrict__ QS, OT *vol, int have_mm)
 {
@@ -1074,18 +1074,22 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
         const dm_f2 x23 = __builtin_elementwise_fma(e23, i23, q23);
         v[0][tw] = (OT)x01.x; v[1][tw] = (OT)x01.y; v[2][tw] = (OT)x23.x; v[3][tw] = (OT)x23.y;
     };
-    if constexpr (TR) {
-        // 1-KB stores: RB rows of NCG 256-B column groups are four consecutive 256-B chunks of
-        // each patch map.  Lane group g computed chunk i of its own patches (g, r); a 4 x 4
-        // transpose over the lane groups (permlane32 then permlane16 swaps, per dword) leaves
-        // lane group g with chunk g of patch (s, r) in X[r][s], so one store instruction writes
-        // 1 KB of ONE map (the maps' rows are consecutive) instead of 256 B of four.
-        constexpr int NCG = G / CH, RB = 4 / NCG;
-        static_assert(CH * sizeof(OT) == 16 && NCG <= 4 && 4 % NCG == 0, "1-KB bursts need 16-B lanes");
+    if constexpr (TR > 0) {
+        // Runs of TR 256-B chunks: RB rows of NCG 256-B column groups are TR consecutive chunks
+        // of each patch map (the maps' rows are consecutive).  Lane group g computed chunk i of
+        // its own patches (g, r).  TR = 4: a 4 x 4 transpose over the lane groups (permlane32
+        // then permlane16 swaps, per dword) leaves lane group g with chunk g of patch (s, r) in
+        // X[r][s], so one store instruction writes 1 KB of ONE map instead of 256 B of four.
+        // TR = 2: the permlane16 stage alone; lane groups 2h, 2h + 1 then hold chunks 0, 1 of
+        // patch (2h + e, r) in X[r][e]: two 512-B runs per store, half the swaps and registers.
+        constexpr int NCG = G / CH, RB = TR / NCG;
+        static_assert((TR == 2 || TR == 4) && CH * sizeof(OT) == 16 && NCG <= TR && TR % NCG == 0,
+                      "runs of 256-B chunks need 16-B lanes");
         OT *const pb = vol + (tb + (size_t)(2 * I0) * W0 + 2 * J0) * (size_t)P;   // patch (0, 0)
-        const int loff = grp * 16 * CH + GW * c;
+        const int sel = TR == 4 ? 0 : grp >> 1;         // TR = 2: the patch pair of this lane
+        const int loff = (grp % TR) * 16 * CH + GW * c;
         for (int q0 = 0; q0 < h0; q0 += RB) {
-            dm_v4i X[4][4];   // [r][i]: chunk i = k NCG + j of the burst, patch (grp, r)
+            dm_v4i X[4][TR];   // [r][i]: chunk i = k NCG + j of the burst, patch (grp, r)
 #pragma unroll
             for (int k = 0; k < RB; ++k) {
                 const int q = q0 + k;
@@ -1105,14 +1109,16 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
             for (int r = 0; r < 4; ++r) {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
+                    if constexpr (TR == 4) {
 #pragma unroll
-                    for (int a = 0; a < 2; ++a) {   // halves: groups 2, 3 of chunk a <-> groups 0, 1 of chunk a + 2
-                        const auto w = __builtin_amdgcn_permlane32_swap(X[r][a][d], X[r][a + 2][d], false, false);
-                        X[r][a][d] = (int)w[0];
-                        X[r][a + 2][d] = (int)w[1];
+                        for (int a = 0; a < 2; ++a) {   // groups 2, 3 of chunk a <-> groups 0, 1 of chunk a + 2
+                            const auto w = __builtin_amdgcn_permlane32_swap(X[r][a][d], X[r][a + 2][d], false, false);
+                            X[r][a][d] = (int)w[0];
+                            X[r][a + 2][d] = (int)w[1];
+                        }
                     }
 #pragma unroll
-                    for (int a = 0; a < 4; a += 2) { // odd rows of 16 lanes of a <-> even rows of a + 1
+                    for (int a = 0; a < TR; a += 2) { // odd rows of 16 lanes of a <-> even rows of a + 1
                         const auto w = __builtin_amdgcn_permlane16_swap(X[r][a][d], X[r][a + 1][d], false, false);
                         X[r][a][d] = (int)w[0];
                         X[r][a + 1][d] = (int)w[1];
@@ -1122,15 +1128,19 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
 #pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) {
-                    const size_t pofs = (size_t)((2 * (s2 >> 1) + (r >> 1)) * W0 + 2 * (s2 & 1) + (r & 1)) * (size_t)P;
-                    ov *dst = (ov *)(pb + pofs + (size_t)q0 * W0 + loff);
-                    const ov o = __builtin_bit_cast(ov, X[r][s2]);
+                for (int e = 0; e < TR; ++e) {
+                    // TR = 4: patch (e, r); TR = 2: patch (2 sel + e, r)
+                    const int pofs = (2 * (e >> 1) + (r >> 1) + 2 * sel) * W0 + 2 * (e & 1) + (r & 1);
+                    ov *dst = (ov *)(pb + (size_t)pofs * (size_t)P + (size_t)q0 * W0 + loff);
+                    const ov o = __builtin_bit_cast(ov, X[r][e]);
                     if constexpr (NT) __builtin_nontemporal_store(o, dst);
                     else *dst = o;
                 }
             }
-            if (q0 + RB < h0) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+            if (q0 + RB < h0) {
+                if constexpr (TR == 4) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+            }
         }
     } else {
     for (int q0 = 0; q0 < h0; ++q0) {

@@ -377,6 +377,26 @@ def match_levels(levels, sub_pix=True, filtering=False, filter_window_size=3, fi
     return out[0]
 
 
+def subpix_map(level0, match):
+    """Matching._sub_pix_cal (Matching.py:177-209) in place on a map that a descent left at a
+    level above 0: `match` float64 [3][hm][wm] (device), refined against co_map_list[0]
+    (`level0`: [h0][w0][h0][w0] or [h0*w0][h0*w0], host or device) at patch (i, j) and window
+    (row, col) of each entry, as the reference does (dm_subpix_map)."""
+    lib = L.load()
+    dev = match.device
+    l0 = torch.as_tensor(level0, dtype=torch.float64).to(dev).contiguous()
+    if l0.dim() == 4:
+        h0, w0 = l0.shape[:2]
+    else:
+        raise ValueError('level 0 must be [h0][w0][h0][w0]')
+    _, hm, wm = match.shape
+    if not match.is_contiguous() or match.dtype != torch.float64:
+        raise ValueError('match must be a contiguous float64 [3][h][w] tensor')
+    L.check(lib.dm_subpix_map(L.ptr(l0), 1, h0, w0, hm, wm, L.ptr(match), L.stream_handle()),
+            'dm_subpix_map')
+    return match
+
+
 def cal_map(match, mode, stream=None):
     """Calc_difference.cal_map on a [T][3][h][w] (or [3][h][w]) device tensor."""
     if mode not in L.CAL_MODES:

@@ -87,22 +87,25 @@ class Matching():
         lst, bottom, steps = self._descent()
         n = len(lst)
         fnum = self.filtering_num if self.filtering else 0
-        if bottom > 0 and self.sub_pix:
-            # the reference would refine a level-`bottom` map against co_map_list[0]; not
-            # provided (deviations)
-            raise NotImplementedError('Matching: N_map = %d stops the descent at level %d of %d; '
-                                      'sub_pix needs it to reach level 0' % (self.obj.N_map, bottom, n))
+        # a descent that stops above level 0 is refined against co_map_list[0] all the same,
+        # at the coarse map's (i, j, row, col) (:182-186): match without sub-pixel, then
+        # dm_subpix_map on level 0
+        sub_here = self.sub_pix and bottom == 0
         pyr = getattr(lst, 'pyramid', None)
         if isinstance(pyr, engine.DevicePyramid) and bottom == 0:
             out = pyr.match(self.sub_pix, self.filtering, self.filter_window_size, fnum,
                             self.filtering_mode, nlev=n)[0]
         elif isinstance(pyr, engine.DevicePyramid):
             levels = [lst.device(k).reshape(pyr.level_shape(k)) for k in range(bottom, n)]
-            out = engine.match_levels(levels, self.sub_pix, self.filtering, self.filter_window_size,
+            out = engine.match_levels(levels, sub_here, self.filtering, self.filter_window_size,
                                       fnum, self.filtering_mode)
         else:
-            out = engine.match_levels([lst[k] for k in range(bottom, n)], self.sub_pix, self.filtering,
+            out = engine.match_levels([lst[k] for k in range(bottom, n)], sub_here, self.filtering,
                                       self.filter_window_size, fnum, self.filtering_mode)
+        if self.sub_pix and bottom > 0:
+            l0 = lst.device(0).reshape(pyr.level_shape(0)) if isinstance(pyr, engine.DevicePyramid) \
+                else lst[0]
+            engine.subpix_map(l0, out)
         if self.filtering:  # _initial_move_map / _B decrement it once per level (:91-93, :136-138)
             self.filtering_num = max(0, self.filtering_num - (steps + 1))
         return out

@@ -172,6 +172,16 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
              int32_t filter_window, int32_t filter_num, int32_t filter_mode,
              double *d_scratch, double *d_out, void *stream);
 
+/* Matching._sub_pix_cal (Matching.py:177-209) for a descent that stops ABOVE level 0 (an
+ * N_map whose halvings end before the list does, Matching.py:85-96, :133-134): the final
+ * map of a coarser level (float64 [T][3][hm][wm], from dm_match on co_map_list[bottom:]
+ * without sub_pix) is refined in place against the materialised level 0 d_level0 (float64
+ * [T][h0*w0][h0*w0], co_map_list[0]) at patch (i, j) and window (row, col) of each entry, as
+ * the reference does; bounds are level 0's (h0, w0), index -1 wraps as in Python.  hm <= h0,
+ * wm <= w0.  dm_match's own sub_pix is this with hm = h0, wm = w0. */
+int dm_subpix_map(const double *d_level0, int32_t T, int32_t h0, int32_t w0, int32_t hm, int32_t wm,
+                  double *d_map, void *stream);
+
 /* misc/sub_pix_cal.py sub_pix_cal (:22-53): clamp to [-3,3], quadratic refinement of an
  * (h, w) disparity map along `direction` (0 rows, 1 cols) on the score map scaled by
  * `ratio`, reject |delta| > 1, clamp again.  float64 in/out, device pointers. */
@@ -259,11 +269,12 @@ int dm_seq_sum(const double *d_v, int64_t n, double *d_out, void *stream);
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 107 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 108 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
  * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
- * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum). */
+ * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum,
+ * 1.8 dm_subpix_map). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

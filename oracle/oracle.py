@@ -278,6 +278,16 @@ def match(levels, sub_pix=True, filtering=False, filter_window_size=3, filtering
     return _match_filtered(levels, sub_pix, filter_window_size, filtering_num, filtering_mode)
 
 
+def match_from(levels, bottom, sub_pix=True, filtering=False, filter_window_size=3, filtering_num=3,
+               filtering_mode='median'):
+    """Matching()() with an N_map that stops the descent at level `bottom` (Matching.py:85-96,
+    :133-134): the descent on levels[bottom:], then (sub_pix) _sub_pix_cal of that coarse map
+    against levels[0] (Matching.py:177-209)."""
+    mp = match(levels[bottom:], sub_pix=False, filtering=filtering, filter_window_size=filter_window_size,
+               filtering_num=filtering_num, filtering_mode=filtering_mode)
+    return _sub_pix(mp, levels[0]) if sub_pix else mp
+
+
 def _near(M, pd0, pd1):
     h, w = M.shape
     win = np.zeros((3, 3))
@@ -322,11 +332,14 @@ def _match_filtered(levels, sub_pix, fw, fnum, fmode):
 
 
 def _sub_pix(mp, L0):
+    """Matching._sub_pix_cal (Matching.py:177-209): the map may be a coarser level's (a
+    descent that stops above level 0); co_map_list[0] is read at (i, j, row, col) of each
+    entry and the bounds are level 0's window sides."""
     def comp(r0, r1, r_):
         return -(r1 - r_) / (2 * (r1 + r_ - 2 * r0)) if (r0 > r1 and r0 > r_) else 0
-    h0, w0 = mp.shape[1:]
-    for i in range(h0):
-        for j in range(w0):
+    h0, w0 = L0.shape[2:]
+    for i in range(mp.shape[1]):
+        for j in range(mp.shape[2]):
             c0, c1 = int(mp[0, i, j]), int(mp[1, i, j])
             d_x = i - mp[0, i, j]
             if c0 + 1 >= h0:

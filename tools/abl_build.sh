@@ -7,14 +7,20 @@
 #   pnoread pow14_zf without its LDS table reads (values from the index bits, no LDS)
 #   prow    c_i and a float32 (1/c_i)^y lo packed into the fp row: one b128 read instead of
 #           b128 + b32 (a layout probe: the row's contents are not rebuilt)
-#   vtr     k_volume_ls with its 1-KB transposed stores (DM_VOLUME_TR 1; results exact)
+#   h2n, h2p, h4p, h0p   the w0 = 128 binary16 volume with the min/max known: runs of 2 / 4
+#           256-B chunks per store (transposed across lane groups) or none, nontemporal (n) or
+#           plain (p) stores (DM_VL_H_*; results exact)
+#   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
+#           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
+#   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
+#           instead of 4 (DM_C2_NB; results exact)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
 REPO=$(cd "$(dirname "$0")/.." && pwd)
 FLAGS="-O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wno-pass-failed -mllvm -amdgpu-mfma-vgpr-form --offload-arch=gfx950"
 for v in "$@"; do
-  r=/tmp/abl_$v; rm -rf $r; d=$r/pkg; mkdir -p $d; cp -r $REPO/deepmatching_stereo_matching_amd/csrc $d/; cp -r $REPO/include $r/
+  EXTRA=""; r=/tmp/abl_$v; rm -rf $r; d=$r/pkg; mkdir -p $d; cp -r $REPO/deepmatching_stereo_matching_amd/csrc $d/; cp -r $REPO/include $r/
   case $v in
     nobar) sed -i '628s/__syncthreads();/__builtin_amdgcn_wave_barrier();/' $d/csrc/dm_mfma.h ;;
     nopow) python3 - $d/csrc/dm_kernels.hip <<'PY'
@@ -59,12 +65,21 @@ s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
     ;;
-    vtr) sed -i 's/^#define DM_VOLUME_TR 0$/#define DM_VOLUME_TR 1/' $d/csrc/dm_kernels.hip
-         grep -q '^#define DM_VOLUME_TR 1$' $d/csrc/dm_kernels.hip || { echo "vtr patch failed"; exit 1; } ;;
+    h2n) EXTRA="-DDM_VL_H_TR=2" ;;
+    h2p) EXTRA="-DDM_VL_H_TR=2 -DDM_VL_H_NT=0" ;;
+    h4p) EXTRA="-DDM_VL_H_TR=4 -DDM_VL_H_NT=0" ;;
+    h0p) EXTRA="-DDM_VL_H_NT=0" ;;
+    f4m) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_MW=4" ;;
+    f4mp) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_MW=4 -DDM_VL_F_NT=0" ;;
+    f2mp) EXTRA="-DDM_VL_F_TR=2 -DDM_VL_F_MW=4 -DDM_VL_F_NT=0" ;;
+    f4p) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_NT=0" ;;
+    f0p) EXTRA="-DDM_VL_F_NT=0" ;;
+    c2nb2) EXTRA="-DDM_C2_NB=2" ;;
+    c2nb8) EXTRA="-DDM_C2_NB=8" ;;
     base) ;;
     *) echo "unknown $v"; exit 2 ;;
   esac
-  (cd $d && /opt/rocm/bin/hipcc $FLAGS -I $r/include csrc/dm_kernels.hip csrc/dm_postproc.hip -o $REPO/ab/libdm_$v.so) &
+  (cd $d && /opt/rocm/bin/hipcc $FLAGS $EXTRA -I $r/include csrc/dm_kernels.hip csrc/dm_postproc.hip -o $REPO/ab/libdm_$v.so) &
 done
 wait
 ls -la $REPO/ab

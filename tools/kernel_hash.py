@@ -20,7 +20,7 @@ EM_AMDGPU = 224
 
 # the kernel instance each profiled shape launches (mangled-name substrings, unique in the
 # library): (kind, tile, bytes per voxel or None) -> symbol
-LEVEL = {64: 'k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi2ELb1EE',      # C2: NB = 2 blocks per workgroup
+LEVEL = {64: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',      # C2: NB = 4 blocks per workgroup
          128: 'k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi1ELb1EE',     # C3: GW = 4, 2 waves
          256: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}     # C5: GW = 4, 4 waves
 VOLUME = {(128, 4): 'k_volume_lsILi8ELi8ELb1EfL', (128, 2): 'k_volume_lsILi8ELi8ELb1EDF16_L',

@@ -11,13 +11,3 @@ for pass in 1 2; do
   done
 done
 timeout -k 10 120 ./tools/store_probe.bin c3_f16 c3_f32 c5_f16 > ${O}_store.jsonl 2>&1 || exit 1
-# k_volume_ls with 1-KB transposed stores (ab/libdm_vtr.so): parity, then A/B
-DM_LIB_PATH=$PWD/ab/libdm_vtr.so timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v -k "volume" --timeout 120 --timeout-method thread > ${O}_vtr_test.log 2>&1 || exit 1
-for pass in 1 2; do
-  for lib in $L ab/libdm_vtr.so; do
-    for a in "--f16" "--f16 --mm" "" "--mm" "--f16 --tile 256 --tiles 8" "--tile 256 --tiles 4"; do
-      echo "== pass $pass $lib $a" >> ${O}_vtr.txt
-      DM_LIB_PATH=$PWD/$lib timeout -k 10 120 python3 tools/vbench.py --tiles 64 $a --rounds 3 >> ${O}_vtr.txt 2>&1 || exit 1
-    done
-  done
-done

@@ -9,6 +9,7 @@
 //   volx  : k_volume_ls's patches and order, but each store instruction 1 KB of ONE patch map
 //           (lane group g writes the map's 256-B chunk 4k + g): the pattern a cross-lane-group
 //           transpose of four rows' results would give
+//   volh  : the same with 2 x 512 B per instruction (two lane groups per map)
 // each with plain or nontemporal stores, 8 waves per workgroup as k_volume_ls.  No arithmetic:
 // the rate each pattern allows the write path.  One JSON line per shape on stdout.
 //   hipcc -O3 --offload-arch=gfx950 tools/store_probe.hip -o tools/store_probe.bin
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(512) void k_vol(char *vol, int S, int esz)
     }
 }
 
-template <bool NT>
+template <bool NT, int RUN = 4>
 __global__ __launch_bounds__(512) void k_volx(char *vol, int S, int esz)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -78,12 +79,15 @@ __global__ __launch_bounds__(512) void k_volx(char *vol, int S, int esz)
     const int I0 = 2 * (int)(bi / (S / 4)), J0 = 2 * (int)(bi % (S / 4));
     const v4u v = {(unsigned)lane, 1u, 2u, 3u};
     const int chunks = (int)(mapb / 256);
-    for (int q = 0; q < chunks; q += 4) {
+    // RUN = 4: lane group g writes chunk q + g of patch pp (1 KB of one map per instruction);
+    // RUN = 2: lane groups 2h, 2h + 1 write chunks q, q + 1 of patch (pp + h) (2 x 512 B)
+    for (int q = 0; q < chunks; q += RUN) {
 #pragma unroll
-        for (int pp = 0; pp < 16; ++pp) {
-            const int g = pp >> 2, r = pp & 3;
+        for (int pp = 0; pp < 16; pp += 4 / RUN) {
+            const int pq = RUN == 4 ? pp : pp + (grp >> 1);
+            const int g = pq >> 2, r = pq & 3;
             const size_t p = (size_t)(2 * (I0 + (g >> 1)) + (r >> 1)) * S + 2 * (J0 + (g & 1)) + (r & 1);
-            st16<NT>(vol + (t * P + p) * mapb + (size_t)(q + grp) * 256 + c * 16, v);
+            st16<NT>(vol + (t * P + p) * mapb + (size_t)(q + (grp % RUN)) * 256 + c * 16, v);
         }
     }
 }
@@ -151,6 +155,8 @@ int main(int argc, char **argv)
         run("vol4_nt", [&] { k_vol<4, true><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("volx", [&] { k_volx<false><<<grid, 512>>>(vol, sh.S, sh.esz); });
         run("volx_nt", [&] { k_volx<true><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("volh", [&] { k_volx<false, 2><<<grid, 512>>>(vol, sh.S, sh.esz); });
+        run("volh_nt", [&] { k_volx<true, 2><<<grid, 512>>>(vol, sh.S, sh.esz); });
         printf("}\n");
         fflush(stdout);
     }

@@ -30,6 +30,7 @@ def main():
     ap.add_argument('--mm', action='store_true',
                     help='min/max already in the stats (one untimed standalone launch first), timed with '
                          'dm_corr_volume_ex(DM_VOLUME_MINMAX_KNOWN)')
+    ap.add_argument('--checksum', action='store_true', help='print a checksum of the volume bits')
     args = ap.parse_args()
     S, ws = args.tile, 5
     side = 9 * S + ws - 1
@@ -67,6 +68,15 @@ def main():
     gb = vol.element_size() * vol.numel() / 1e9
     for v, ts in res.items():
         print('%-24s median %8.3f ms  %7.1f GB/s' % (v, np.median(ts), gb / (np.median(ts) * 1e-3)))
+    if args.checksum:
+        # position-weighted checksum of the last volume's bits, tile by tile on the device: library
+        # builds that A/B a kernel variant print the same value iff their volumes are bit-identical
+        bits = vol.view(torch.int16 if args.f16 else torch.int32).reshape(vol.shape[0], -1)
+        w = torch.arange(1, bits.shape[1] + 1, device=dev, dtype=torch.int64) % 1000003
+        acc = 0
+        for t in range(bits.shape[0]):
+            acc = (acc * 1000033 + int((bits[t].to(torch.int64) * w).sum())) % (1 << 61)
+        print('volume checksum %016x' % acc)
 
 
 if __name__ == '__main__':
