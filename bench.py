@@ -290,10 +290,10 @@ def load_pmc(tile, kernel='level1', tiles=None):
     return {}
 
 
-def isa_check(d, key, kind, tile, esz=None):
+def isa_check(d, key, kind, tile, esz=None, mm=False):
     """Does profile field `key` (an ISA hash recorded when the profile was made) name the kernel
     bytes of the library this process loaded?  -> (ok, note)."""
-    sym = kernel_hash.symbol(kind, tile, esz)
+    sym = kernel_hash.symbol(kind, tile, esz, mm)
     cur = kernel_hash.kernel_hash(sym) if sym else None
     rec = d.get(key)
     if cur is None:
@@ -309,7 +309,8 @@ def load_traffic(tile, kernel='level1', tiles=None):
     on the kernel bytes this process loaded."""
     d = load_pmc(tile, kernel, tiles)
     esz = 2 if 'f16' in kernel else 4
-    ok, _ = isa_check(d, 'isa_sha16', 'level' if kernel == 'level1' else 'volume', tile, esz)
+    ok, _ = isa_check(d, 'isa_sha16', 'level' if kernel == 'level1' else 'volume', tile, esz,
+                      kernel.endswith('_mm'))
     return d.get('hbm_bytes_per_launch') if ok else None
 
 

@@ -1383,6 +1383,9 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
+#ifndef DM_C3_NB
+#define DM_C3_NB 2   // two-wave cell blocks per workgroup of the S = 128 level kernel
+#endif
 #ifndef DM_C2_NB
 #define DM_C2_NB 4   // one-wave cell blocks per workgroup of the S = 64 level kernel
 #endif
@@ -1417,7 +1420,10 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     // GW = 4 with 2 waves (C3): 20 KB of LDS (the exchange arrays in the pow tables' hole)
     // allow 8 workgroups per CU, so a 4 waves/SIMD register budget (<= 128 VGPRs)
     if (KS == 1 && GW == 4 && NW == 2) {
-        k_level1_mfq<1, 4, 2, 4, L2F, YF, 1, CL><<<grid, 64 * 2, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        constexpr int NBc = DM_C3_NB;
+        const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
+        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1448,20 +1454,27 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 // LDS-shared-window volume kernel (k_volume_ls): ws <= 5 on the MFMA shapes, 8 waves (patch
 // blocks) per workgroup, nontemporal stores
 // The w0 = 128 (C3) instances: store runs (TR), register budget (waves per SIMD, MW) and
-// nontemporal stores (NT) per output type, chosen by same-box A/B.
-// binary16 with the min/max known (no min/max sweep):
+// nontemporal stores (NT) per output type, chosen by same-box A/B with bit-identical output
+// (profiles/r04h_vol.txt, volume checksums; r04g_vtr.txt).  binary16 with the min/max known
+// (no min/max sweep): 2 x 512-B runs per store, 144 VGPRs, 6.78 -> 6.61-6.69 ms on 64 tiles
+// (6.75 -> 6.42-6.46 on a second box); 1-KB runs (194 VGPRs) 6.94-6.99, plain stores 9.1-9.3
+// (the window loads then compete with write-allocate traffic).  The standalone binary16
+// volume keeps 256-B runs: its min/max sweep needs the occupancy (runs of 2 / 4: 8.8-9.1 ms
+// against 7.85-7.94).
 #ifndef DM_VL_H_TR
-#define DM_VL_H_TR 0
+#define DM_VL_H_TR 2
 #endif
 #ifndef DM_VL_H_NT
 #define DM_VL_H_NT 1
 #endif
-// float32:
+// float32: 1-KB runs compiled for 4 waves per SIMD (128 VGPRs, 4 spilled) 14.27 -> 13.60-13.71 ms
+// standalone, 13.69 -> 13.07-13.11 ms with the min/max known; 1-KB runs at 186 VGPRs 14.0 /
+// 16.5 (plain), 2 x 512 B 14.1-14.3.
 #ifndef DM_VL_F_TR
-#define DM_VL_F_TR 0
+#define DM_VL_F_TR 4
 #endif
 #ifndef DM_VL_F_MW
-#define DM_VL_F_MW 1
+#define DM_VL_F_MW 4
 #endif
 #ifndef DM_VL_F_NT
 #define DM_VL_F_NT 1

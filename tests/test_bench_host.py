@@ -24,10 +24,11 @@ def test_every_profiled_kernel_is_in_the_library():
     hashes = {}
     for tile in K.LEVEL:
         hashes[('level', tile)] = K.kernel_hash(K.symbol('level', tile))
-    for tile, esz in K.VOLUME:
-        hashes[('volume', tile, esz)] = K.kernel_hash(K.symbol('volume', tile, esz))
+    for tile, esz, mm in K.VOLUME:
+        hashes[('volume', tile, esz, mm)] = K.kernel_hash(K.symbol('volume', tile, esz, mm))
     assert all(h and len(h) == 16 for h in hashes.values()), hashes
-    assert len(set(hashes.values())) == len(hashes)          # distinct instances
+    syms = {K.symbol(*k) for k in hashes}
+    assert len(set(hashes.values())) == len(syms)            # one hash per distinct instance
     assert K.kernel_hash('no_such_kernel') is None
     assert K.kernel_hash('k_level1_mfq') is None             # ambiguous: many instances
 
@@ -72,5 +73,6 @@ def test_volume_traffic_needs_a_current_profile(bench, monkeypatch):
     monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {'hbm_bytes_per_launch': 35e9, 'isa_sha16': cur})
     assert bench.load_traffic(128, 'volume_f16', 64) == 35e9
     assert bench.load_traffic(128, 'volume', 64) is None     # float32 instance: other bytes
+    assert bench.load_traffic(128, 'volume_f16_mm', 64) is None   # min/max-known instance
     monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {'hbm_bytes_per_launch': 35e9})
     assert bench.load_traffic(128, 'volume_f16', 64) is None

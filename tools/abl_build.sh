@@ -14,6 +14,8 @@
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
 #           instead of 4 (DM_C2_NB; results exact)
+#   c3nb2, c3nb4   the S = 128 level kernel with 2 / 4 two-wave cell blocks per workgroup
+#           instead of 1 (DM_C3_NB; results exact)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -75,6 +77,8 @@ PY
     f4p) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_NT=0" ;;
     f0p) EXTRA="-DDM_VL_F_NT=0" ;;
     c2nb2) EXTRA="-DDM_C2_NB=2" ;;
+    c3nb2) EXTRA="-DDM_C3_NB=2" ;;
+    c3nb4) EXTRA="-DDM_C3_NB=4" ;;
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
     base) ;;
     *) echo "unknown $v"; exit 2 ;;

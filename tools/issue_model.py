@@ -24,7 +24,7 @@ import isa_cost  # noqa: E402
 import kernel_hash  # noqa: E402
 
 KERNELS = {  # shape -> (kernel symbol substring, weights file, pmc file, waves per launch)
-    'c3': ('k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi1ELb1EE', 'issue_model_level1_c3_weights.json',
+    'c3': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE', 'issue_model_level1_c3_weights.json',
            'pmc_level1.json', 64 * (128 // 4) * (128 // 4) * 2),
     'c2': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE', 'issue_model_level1_c2_weights.json',
            'pmc_level1_s64.json', 64 * (64 // 4) * (64 // 4)),

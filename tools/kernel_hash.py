@@ -20,17 +20,24 @@ EM_AMDGPU = 224
 
 # the kernel instance each profiled shape launches (mangled-name substrings, unique in the
 # library): (kind, tile, bytes per voxel or None) -> symbol
-LEVEL = {64: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',      # C2: NB = 4 blocks per workgroup
-         128: 'k_level1_mfqILi1ELi4ELi2ELi4ELb1ELb1ELi1ELb1EE',     # C3: GW = 4, 2 waves
+LEVEL = {64: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',      # C2: 4 one-wave blocks per workgroup
+         128: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE',     # C3: GW = 4, 2 two-wave blocks
          256: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}     # C5: GW = 4, 4 waves
-VOLUME = {(128, 4): 'k_volume_lsILi8ELi8ELb1EfL', (128, 2): 'k_volume_lsILi8ELi8ELb1EDF16_L',
-          (256, 4): 'k_volume_lsILi16ELi8ELb1EfL', (256, 2): 'k_volume_lsILi16ELi8ELb1EDF16_L'}
+# k_volume_ls<G, NW, NT, OT, TR, MW>: (tile, bytes per voxel, min/max known) -> instance
+# (dm_kernels.hip launch_volume_ls: DM_VL_H_* / DM_VL_F_* at w0 = 128, TR 0 elsewhere)
+VOLUME = {(128, 4, False): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E', (128, 4, True): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E',
+          (128, 2, False): 'k_volume_lsILi8ELi8ELb1EDF16_Li0ELi1E',
+          (128, 2, True): 'k_volume_lsILi8ELi8ELb1EDF16_Li2ELi1E',
+          (256, 4, False): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E', (256, 4, True): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E',
+          (256, 2, False): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E',
+          (256, 2, True): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E'}
 
 
-def symbol(kind, tile, esz=None):
+def symbol(kind, tile, esz=None, mm=False):
     """The symbol substring of the level kernel ('level') or a volume kernel ('volume', esz
-    bytes per voxel) that a tile of side `tile` launches; None if not profiled."""
-    return LEVEL.get(tile) if kind == 'level' else VOLUME.get((tile, esz))
+    bytes per voxel, min/max known or not) that a tile of side `tile` launches; None if not
+    profiled."""
+    return LEVEL.get(tile) if kind == 'level' else VOLUME.get((tile, esz, bool(mm)))
 
 
 def _elfs(data):

@@ -96,7 +96,7 @@ def main(root):
         # the ISA these counters were taken on (the library the passes loaded): bench.py uses
         # the figures only while its loaded library holds the same kernel bytes
         sym = (kernel_hash.symbol('level', tile) if prefix == 'k_level1_mfq'
-               else kernel_hash.symbol('volume', tile, 2 if f16 else 4))
+               else kernel_hash.symbol('volume', tile, 2 if f16 else 4, mm))
         d['isa_symbol'] = sym
         d['isa_sha16'] = kernel_hash.kernel_hash(sym) if sym else None
         if sq:
