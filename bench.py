@@ -222,7 +222,7 @@ def volume_roofline(solver, reps=3, f16=False):
                 'ms': round(ms_k, 3), 'achieved': round(gbs_k, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(gbs_k / HBM_PEAK_GBS, 4),
                 'traffic': load_traffic(batch.h0, key + '_mm', batch.T),
-                'store_pattern_ceiling': store_ceiling(batch.h0, batch.T, esz, gbs_k)}}
+                'store_pattern_ceiling': store_ceiling(batch.h0, batch.T, esz, gbs_k, mm=True)}}
 
 
 def fp16_flip_rate(solver, tiles=2):
@@ -314,23 +314,28 @@ def load_traffic(tile, kernel='level1', tiles=None):
     return d.get('hbm_bytes_per_launch') if ok else None
 
 
-def store_ceiling(tile, tiles, esz, gbs):
-    """The rate the volume kernels' own store pattern allows with no arithmetic
+def store_ceiling(tile, tiles, esz, gbs, mm=False):
+    """The rate the volume kernel's own store pattern allows with no arithmetic
     (tools/store_probe.hip, profiles/store_probe.jsonl: the same volume, 16-B nontemporal
-    stores, 4 x 256 B per instruction into 4 patch maps advancing a row at a time) and the
-    fraction of it this run reached; None for shapes the probe did not run."""
+    stores per lane, the kernel's patches per wave) and the fraction of it this run reached;
+    None for shapes the probe did not run.  The pattern is the instance's (dm_kernels.hip
+    launch_volume_ls): w0 = 128 binary16 with the min/max known stores 2 x 512 B of two patch
+    maps per instruction ("volh_nt"), w0 = 128 float32 1 KB of one map ("volx_nt"), the others
+    4 x 256 B of four maps advancing a row at a time ("vol_nt")."""
     name = 'c%d_f%d' % (3 if tile == 128 else 5, 8 * esz)
+    pattern = ('volh_nt' if tile == 128 and esz == 2 and mm else
+               'volx_nt' if tile == 128 and esz == 4 else 'vol_nt')
     try:
         with open(os.path.join(REPO, 'profiles', 'store_probe.jsonl')) as f:
             rows = [json.loads(ln) for ln in f if ln.strip()]
     except OSError:
         return None
     for r in rows:
-        if r.get('shape') == name and r.get('tiles') == tiles:
-            c = r['vol_nt']['gb_s']
+        if r.get('shape') == name and r.get('tiles') == tiles and pattern in r:
+            c = r[pattern]['gb_s']
             return {'gb_s': c, 'frac': round(gbs / c, 4), 'best_pattern_gb_s': r['seq']['gb_s'],
                     'source': 'profile: tools/store_probe.hip (profiles/store_probe.jsonl), pattern '
-                              '"vol_nt"; best_pattern = each wave streaming a contiguous slab'}
+                              '"%s"; best_pattern = each wave streaming a contiguous slab' % pattern}
     return None
 
 

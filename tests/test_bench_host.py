@@ -76,3 +76,16 @@ def test_volume_traffic_needs_a_current_profile(bench, monkeypatch):
     assert bench.load_traffic(128, 'volume_f16_mm', 64) is None   # min/max-known instance
     monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {'hbm_bytes_per_launch': 35e9})
     assert bench.load_traffic(128, 'volume_f16', 64) is None
+
+
+def test_store_ceiling_follows_the_instance_pattern(bench):
+    # the w0 = 128 instances store 2 x 512 B (binary16, min/max known) or 1 KB (float32) per
+    # instruction; the others 4 x 256 B -- each line is priced against its own pattern
+    h_mm = bench.store_ceiling(128, 64, 2, 5000.0, mm=True)
+    h = bench.store_ceiling(128, 64, 2, 5000.0)
+    f = bench.store_ceiling(128, 64, 4, 5000.0)
+    c5 = bench.store_ceiling(256, 8, 2, 5000.0, mm=True)
+    assert '"volh_nt"' in h_mm['source'] and '"vol_nt"' in h['source']
+    assert '"volx_nt"' in f['source'] and '"vol_nt"' in c5['source']
+    assert h_mm['frac'] == round(5000.0 / h_mm['gb_s'], 4)
+    assert bench.store_ceiling(64, 64, 2, 5000.0) is None
