@@ -1467,6 +1467,9 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 #ifndef DM_VL_H_NT
 #define DM_VL_H_NT 1
 #endif
+#ifndef DM_VL_H_NW
+#define DM_VL_H_NW 4   // waves (16-patch blocks) per workgroup: 144 VGPRs allow 3 four-wave
+#endif          // workgroups per CU against 1 of 8 waves: 6.81 -> 6.52-6.54 ms (r04q_vol_nw.txt); 2 waves 6.66
 // float32: 1-KB runs compiled for 4 waves per SIMD (128 VGPRs, 4 spilled) 14.27 -> 13.60-13.71 ms
 // standalone, 13.69 -> 13.07-13.11 ms with the min/max known; 1-KB runs at 186 VGPRs 14.0 /
 // 16.5 (plain), 2 x 512 B 14.1-14.3.
@@ -1501,7 +1504,10 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
     if (G == 8) {
         if constexpr (sizeof(OT) == 2) {
             if (have_mm) {
-                k_volume_ls<8, 8, DM_VL_H_NT, OT, DM_VL_H_TR><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+                constexpr int NWh = DM_VL_H_NW;
+                if (bpt % NWh) return DM_ERR_UNSUPPORTED;
+                k_volume_ls<8, NWh, DM_VL_H_NT, OT, DM_VL_H_TR><<<(unsigned)(b->T * bpt / NWh), 64 * NWh, 0, st>>>(
+                    gg, s, Bw, QS, out, have_mm);
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }

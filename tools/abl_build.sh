@@ -9,7 +9,7 @@
 #           b128 + b32 (a layout probe: the row's contents are not rebuilt)
 #   h2n, h2p, h4p, h0p   the w0 = 128 binary16 volume with the min/max known: runs of 2 / 4
 #           256-B chunks per store (transposed across lane groups) or none, nontemporal (n) or
-#           plain (p) stores (DM_VL_H_*; results exact)
+#           plain (p) stores (DM_VL_H_*; results exact); h2w8 / h2w2: 8 / 2 waves per workgroup (4 in-tree)
 #   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
@@ -71,6 +71,8 @@ PY
     h2p) EXTRA="-DDM_VL_H_TR=2 -DDM_VL_H_NT=0" ;;
     h4p) EXTRA="-DDM_VL_H_TR=4 -DDM_VL_H_NT=0" ;;
     h0p) EXTRA="-DDM_VL_H_NT=0" ;;
+    h2w8) EXTRA="-DDM_VL_H_NW=8" ;;
+    h2w2) EXTRA="-DDM_VL_H_NW=2" ;;
     f4m) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_MW=4" ;;
     f4mp) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_MW=4 -DDM_VL_F_NT=0" ;;
     f2mp) EXTRA="-DDM_VL_F_TR=2 -DDM_VL_F_MW=4 -DDM_VL_F_NT=0" ;;

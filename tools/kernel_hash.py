@@ -27,7 +27,7 @@ LEVEL = {64: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',      # C2: 4 one-
 # (dm_kernels.hip launch_volume_ls: DM_VL_H_* / DM_VL_F_* at w0 = 128, TR 0 elsewhere)
 VOLUME = {(128, 4, False): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E', (128, 4, True): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E',
           (128, 2, False): 'k_volume_lsILi8ELi8ELb1EDF16_Li0ELi1E',
-          (128, 2, True): 'k_volume_lsILi8ELi8ELb1EDF16_Li2ELi1E',
+          (128, 2, True): 'k_volume_lsILi8ELi4ELb1EDF16_Li2ELi1E',
           (256, 4, False): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E', (256, 4, True): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E',
           (256, 2, False): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E',
           (256, 2, True): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E'}
