@@ -947,20 +947,30 @@ __device__ __forceinline__ void match_step_l1_at(const Geo &g, const Stats &s, i
         }
     }
     // the 9 window sums: every lane of the entry's quad gets all four children (DPP quad
-    // broadcasts, in ul, ur, ll, lr order); lane ch then rectifies the sums of positions
-    // k = ch, ch + 4, ch + 8 only -- 3 sum pows per lane instead of 9 -- and lane 0 collects
-    // the window (out-of-range positions: 0, Matching's zero padding)
-    double mine[3] = {0.0, 0.0, 0.0};
+    // broadcasts, in ul, ur, ll, lr order) and forms every sum; lane ch then rectifies the sums
+    // of positions k = ch, ch + 4 (selected per lane, so the wave issues 2 sum-pows, not 8) and
+    // every lane that of k = 8; lane 0 collects the window (out-of-range positions: 0,
+    // Matching's zero padding)
+    double sk[9];
+    bool ink[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
         const int a = k / 3, b = k % 3;
         const int u = pd0 - 1 + a, v = pd1 - 1 + b;
         double pv = 0.0;
-        const bool in = u >= 0 && u < h1 && v >= 0 && v < w1;
-        if (in) pv = pow14((double)norm_x(r_of_y(R[a][b], ap, g.method), rmn, rmx));
+        ink[k] = u >= 0 && u < h1 && v >= 0 && v < w1;
+        if (ink[k]) pv = pow14((double)norm_x(r_of_y(R[a][b], ap, g.method), rmn, rmx));
         const double v0 = quad_bcast<0>(pv), v1 = quad_bcast<1>(pv), v2 = quad_bcast<2>(pv), v3 = quad_bcast<3>(pv);
-        if ((k & 3) == ch && in) mine[k >> 2] = pow14((((v0 + v1) + v2) + v3) / 4.0);
+        sk[k] = (((v0 + v1) + v2) + v3) / 4.0;
     }
+    double mine[3];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const double x = ch == 0 ? sk[4 * m] : ch == 1 ? sk[4 * m + 1] : ch == 2 ? sk[4 * m + 2] : sk[4 * m + 3];
+        const bool in = ch == 0 ? ink[4 * m] : ch == 1 ? ink[4 * m + 1] : ch == 2 ? ink[4 * m + 2] : ink[4 * m + 3];
+        mine[m] = in ? pow14(x) : 0.0;
+    }
+    mine[2] = ink[8] ? pow14(sk[8]) : 0.0;
     double win[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -1259,6 +1269,7 @@ static inline unsigned nblk(size_t n, unsigned bs)
 // a retiring level-kernel wave leaves (a 4-wave workgroup needs a free slot on every SIMD of a
 // CU at once): the pipelined C3 bench -0.35 % per pair, same box (profiles/r03z2_tail.txt).
 static constexpr unsigned TAIL_WG = 64u;
+
 
 // the last _B step (onto level 0) with level 0 on demand, patch taps in registers
 template <int WS>

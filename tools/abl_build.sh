@@ -12,6 +12,7 @@
 #           plain (p) stores (DM_VL_H_*; results exact); h2w8 / h2w2: 8 / 2 waves per workgroup (4 in-tree)
 #   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
+#   head    the last commit's sources (an A/B of the working tree against it)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
 #           instead of 4 (DM_C2_NB; results exact)
 #   c3nb2, c3nb4   the S = 128 level kernel with 2 / 4 two-wave cell blocks per workgroup
@@ -82,6 +83,9 @@ PY
     c3nb2) EXTRA="-DDM_C3_NB=2" ;;
     c3nb4) EXTRA="-DDM_C3_NB=4" ;;
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
+    head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
+          (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
+             case $f in include/*) git show HEAD:$f > $r/$f ;; *) git show HEAD:$f > $d/csrc/$(basename $f) ;; esac; done) ;;
     base) ;;
     *) echo "unknown $v"; exit 2 ;;
   esac
