@@ -1394,6 +1394,9 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
     return DM_OK;
 }
 
+#ifndef DM_C5_NB
+#define DM_C5_NB 1   // four-wave cell blocks per workgroup of the S = 256 level kernel
+#endif
 #ifndef DM_C3_NB
 #define DM_C3_NB 2   // two-wave cell blocks per workgroup of the S = 128 level kernel
 #endif
@@ -1412,7 +1415,10 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     constexpr bool CL = L2F;
     // GW = 4 with 4 waves (S = 256, C5): 4 waves/SIMD register budget
     if (KS == 1 && GW == 4 && NW == 4) {
-        k_level1_mfq<1, 4, 4, 4, L2F, YF, 1, CL><<<grid, 64 * 4, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        constexpr int NBc = DM_C5_NB;
+        const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
+        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }

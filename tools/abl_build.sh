@@ -15,8 +15,9 @@
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
 #           instead of 4 (DM_C2_NB; results exact)
-#   c3nb2, c3nb4   the S = 128 level kernel with 2 / 4 two-wave cell blocks per workgroup
-#           instead of 1 (DM_C3_NB; results exact)
+#   c3nb1   the S = 128 level kernel with 1 two-wave cell block per workgroup instead of 2
+#   c5nb2   the S = 256 level kernel with 2 four-wave cell blocks per workgroup instead of 1
+#           (DM_C3_NB / DM_C5_NB; results exact)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -80,8 +81,8 @@ PY
     f4p) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_NT=0" ;;
     f0p) EXTRA="-DDM_VL_F_NT=0" ;;
     c2nb2) EXTRA="-DDM_C2_NB=2" ;;
-    c3nb2) EXTRA="-DDM_C3_NB=2" ;;
-    c3nb4) EXTRA="-DDM_C3_NB=4" ;;
+    c3nb1) EXTRA="-DDM_C3_NB=1" ;;
+    c5nb2) EXTRA="-DDM_C5_NB=2" ;;
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
     head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
           (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
