@@ -1490,6 +1490,19 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 // float32: 1-KB runs compiled for 4 waves per SIMD (128 VGPRs, 4 spilled) 14.27 -> 13.60-13.71 ms
 // standalone, 13.69 -> 13.07-13.11 ms with the min/max known; 1-KB runs at 186 VGPRs 14.0 /
 // 16.5 (plain), 2 x 512 B 14.1-14.3.
+// w0 = 256 (C5): binary16 with the min/max known, float32 (A/B switches, 256-B runs by default)
+#ifndef DM_VL_H2_TR
+#define DM_VL_H2_TR 0
+#endif
+#ifndef DM_VL_H2_NW
+#define DM_VL_H2_NW 8
+#endif
+#ifndef DM_VL_F2_TR
+#define DM_VL_F2_TR 0
+#endif
+#ifndef DM_VL_F2_MW
+#define DM_VL_F2_MW 1
+#endif
 #ifndef DM_VL_F_TR
 #define DM_VL_F_TR 4
 #endif
@@ -1530,6 +1543,22 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
             }
         } else {
             k_volume_ls<8, 8, DM_VL_F_NT, OT, DM_VL_F_TR, DM_VL_F_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+            HIP_TRY(hipGetLastError());
+            return DM_OK;
+        }
+    }
+    if (G == 16) {   // w0 = 256 (C5)
+        if constexpr (sizeof(OT) == 2) {
+            if (have_mm) {
+                constexpr int NWh = DM_VL_H2_NW;
+                if (bpt % NWh) return DM_ERR_UNSUPPORTED;
+                k_volume_ls<16, NWh, true, OT, DM_VL_H2_TR><<<(unsigned)(b->T * bpt / NWh), 64 * NWh, 0, st>>>(
+                    gg, s, Bw, QS, out, have_mm);
+                HIP_TRY(hipGetLastError());
+                return DM_OK;
+            }
+        } else {
+            k_volume_ls<16, 8, true, OT, DM_VL_F2_TR, DM_VL_F2_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
             HIP_TRY(hipGetLastError());
             return DM_OK;
         }

@@ -76,8 +76,9 @@ def _symbols(data, base):
 
 
 def kernel_hash(symbol_substring, lib=None):
-    """sha256 (hex, 16 chars) of the machine code + kernel descriptor of the ONE kernel whose
-    mangled name contains `symbol_substring`; None if the library or the kernel is absent."""
+    """sha256 (hex, 16 chars) of the machine code + kernel descriptor (less its code offset) of
+    the ONE kernel whose mangled name contains `symbol_substring`; None if the library or the
+    kernel is absent."""
     lib = lib or os.environ.get('DM_LIB_PATH') or os.path.join(
         REPO, 'deepmatching_stereo_matching_amd', 'libdmstereo.so')
     try:
@@ -92,7 +93,12 @@ def kernel_hash(symbol_substring, lib=None):
                 kd = syms.get(nm + '.kd')
                 h = hashlib.sha256(data[off:off + size])
                 if kd:
-                    h.update(data[kd[0]:kd[0] + kd[1]])
+                    # the descriptor without kernel_code_entry_byte_offset (bytes 16-23): that
+                    # field is where the linker put the code relative to the descriptor, which
+                    # moves whenever another kernel of the library is added or grows
+                    d = bytearray(data[kd[0]:kd[0] + kd[1]])
+                    d[16:24] = bytes(8)
+                    h.update(bytes(d))
                 found.append((nm, h.hexdigest()[:16]))
     if len(found) != 1:
         return None

@@ -72,10 +72,14 @@ def main():
         # position-weighted checksum of the last volume's bits, tile by tile on the device: library
         # builds that A/B a kernel variant print the same value iff their volumes are bit-identical
         bits = vol.view(torch.int16 if args.f16 else torch.int32).reshape(vol.shape[0], -1)
-        w = torch.arange(1, bits.shape[1] + 1, device=dev, dtype=torch.int64) % 1000003
+        CH = 1 << 26   # elements per chunk (an S = 256 tile holds 2^32)
+        base = torch.arange(CH, device=dev, dtype=torch.int64)
         acc = 0
         for t in range(bits.shape[0]):
-            acc = (acc * 1000033 + int((bits[t].to(torch.int64) * w).sum())) % (1 << 61)
+            for o in range(0, bits.shape[1], CH):
+                part = bits[t, o:o + CH].to(torch.int64)
+                w = (base[:part.numel()] + (o + 1)) % 1000003
+                acc = (acc * 1000033 + int((part * w).sum())) % (1 << 61)
         print('volume checksum %016x' % acc)
 
 
