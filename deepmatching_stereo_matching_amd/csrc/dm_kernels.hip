@@ -1503,6 +1503,12 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 #ifndef DM_VL_F2_MW
 #define DM_VL_F2_MW 1
 #endif
+#ifndef DM_VL_HS_NW
+#define DM_VL_HS_NW 8   // binary16 standalone (w0 = 128): waves per workgroup
+#endif
+#ifndef DM_VL_F_NW
+#define DM_VL_F_NW 8    // float32 (w0 = 128): waves per workgroup
+#endif
 #ifndef DM_VL_F_TR
 #define DM_VL_F_TR 4
 #endif
@@ -1541,8 +1547,18 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
+            if constexpr (DM_VL_HS_NW != 8) {
+                constexpr int NWs = DM_VL_HS_NW;
+                if (bpt % NWs) return DM_ERR_UNSUPPORTED;
+                k_volume_ls<8, NWs, true, OT><<<(unsigned)(b->T * bpt / NWs), 64 * NWs, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+                HIP_TRY(hipGetLastError());
+                return DM_OK;
+            }
         } else {
-            k_volume_ls<8, 8, DM_VL_F_NT, OT, DM_VL_F_TR, DM_VL_F_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+            constexpr int NWf = DM_VL_F_NW;
+            if (bpt % NWf) return DM_ERR_UNSUPPORTED;
+            k_volume_ls<8, NWf, DM_VL_F_NT, OT, DM_VL_F_TR, DM_VL_F_MW><<<(unsigned)(b->T * bpt / NWf), 64 * NWf, 0, st>>>(
+                gg, s, Bw, QS, out, have_mm);
             HIP_TRY(hipGetLastError());
             return DM_OK;
         }

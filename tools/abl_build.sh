@@ -13,6 +13,7 @@
 #   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
+#   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
 #   c5h2w4, c5f4m   the w0 = 256 volumes: binary16 min/max known with 2 x 512-B runs in
 #           4-wave workgroups; float32 with 1-KB runs at 4 waves/SIMD (DM_VL_H2_*, DM_VL_F2_*)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
@@ -82,6 +83,8 @@ PY
     f2mp) EXTRA="-DDM_VL_F_TR=2 -DDM_VL_F_MW=4 -DDM_VL_F_NT=0" ;;
     f4p) EXTRA="-DDM_VL_F_TR=4 -DDM_VL_F_NT=0" ;;
     f0p) EXTRA="-DDM_VL_F_NT=0" ;;
+    hsw4) EXTRA="-DDM_VL_HS_NW=4" ;;
+    fw4) EXTRA="-DDM_VL_F_NW=4" ;;
     c5h2w4) EXTRA="-DDM_VL_H2_TR=2 -DDM_VL_H2_NW=4" ;;
     c5f4m) EXTRA="-DDM_VL_F2_TR=4 -DDM_VL_F2_MW=4" ;;
     c2nb2) EXTRA="-DDM_C2_NB=2" ;;
