@@ -296,8 +296,11 @@ def isa_check(d, key, kind, tile, esz=None, mm=False):
     sym = kernel_hash.symbol(kind, tile, esz, mm)
     cur = kernel_hash.kernel_hash(sym) if sym else None
     rec = d.get(key)
+    if sym is None:
+        return False, 'no profiled kernel instance for this shape'
     if cur is None:
-        return False, 'no ISA hash for this kernel in the loaded library'
+        return False, ('kernel instance %s not found in the loaded library (a non-default build? its '
+                       'dm_build_config: %s)' % (sym, kernel_hash.build_config()))
     if rec != cur:
         return False, ('stale profile: it was made on kernel ISA %s, the loaded library holds %s '
                        '(re-run tools/pmc_r03.sh / tools/issue_model.py)' % (rec, cur))

@@ -49,6 +49,7 @@ _TP = ctypes.POINTER(DmTiles)
 SIGNATURES = {
     'dm_abi_version': ([], ctypes.c_int),
     'dm_last_error': ([], ctypes.c_char_p),
+    'dm_build_config': ([], ctypes.c_char_p),
     'dm_stats_bytes': ([_TP], ctypes.c_size_t),
     'dm_corr_stats': ([_TP, _P, _P], ctypes.c_int),
     'dm_corr_level1': ([_TP, _P, _P, _P], ctypes.c_int),
@@ -64,6 +65,7 @@ SIGNATURES = {
     'dm_match': ([_TP, _P, ctypes.POINTER(ctypes.c_void_p), _I, _I, _I, _I, _I, _I, _I, _I,
                   _P, _P, _P], ctypes.c_int),
     'dm_subpix_map': ([_P, _I, _I, _I, _I, _I, _P, _P], ctypes.c_int),
+    'dm_subpix_map_tiles': ([_TP, _P, _I, _I, _P, _P], ctypes.c_int),
     'dm_sub_pix_cal': ([_P, _P, _I, _I, _I, ctypes.c_double, _P, _P], ctypes.c_int),
     'dm_cal_map': ([_P, _I, _I, _I, _I, _P, _P], ctypes.c_int),
     'dm_gs_schedule': ([_I, _I, _I, _I, _I, _I, _P, _P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),

@@ -1002,8 +1002,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MW))) void 
 // hm x wm: h0 x w0 after a descent to level 0, a coarser level's when the descent stops
 // above it -- the reference still reads co_map_list[0] at (i, j, row, col) of that map
 // (:182-186), so the level-0 patch is (i, j) and the bounds are level 0's window sides.
-// Indices outside [0, h0) x [0, w0) leave the entry as it is (the reference's IndexError
-// branch; a matching descent never produces them).
+// An entry is any float (dm_subpix_map accepts arbitrary maps), indexed the way numpy indexes
+// co_map_list[0][i, j, c0 +- 1, c1] with c = int(value): an index in [-N, N) is valid and a
+// negative one wraps (value + N); any other index raises IndexError, caught by the bare
+// except (:193-194, :205-206), which writes i - d_x (j - d_y).  The row refinement reads
+// (c0 - 1, c1), (c0, c1), (c0 + 1, c1), so it needs c0 in [-h0 + 1, h0 - 2] and c1 in
+// [-w0, w0); the column one c1 in [-w0 + 1, w0 - 2] and c0 in [-h0, h0).  (A NaN or an
+// entry beyond int range makes the reference's int() raise outside the try; here it takes
+// the except branch.)
+__device__ __forceinline__ int py_index(double v)
+{
+    return (v == v && fabs(v) < 1073741824.0) ? (int)v : -0x40000000; // int(): truncation
+}
+
+__device__ __forceinline__ bool py_in(int k, int n) { return k >= -n && k < n; }
+__device__ __forceinline__ int py_wrap(int k, int n) { return k < 0 ? k + n : k; }
+
 __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0, int hm, int wm, double *map)
 {
     DM_TAIL_ENTRY();
@@ -1014,25 +1028,21 @@ __global__ void k_subpix(Geo g, Stats s, const double *L0, int T, int h0, int w0
     const int p0 = pc / wm, p1 = pc % wm;
     double *mt = map + (size_t)t * 3 * Pm;
     const double *M = L0 ? L0 + ((size_t)t * P + (size_t)p0 * w0 + p1) * P : nullptr;
+    // (r_, c_) already wrapped into [0, h0) x [0, w0)
 #define L0V(r_, c_) (M ? M[(size_t)(r_) * w0 + (c_)] : l0_value(g, s, t, p0, p1, (r_), (c_)))
     const double row = mt[pc], col = mt[Pm + pc];
-    const int c0 = (int)row, c1 = (int)col; // int() truncation of exact integers
-    if (!(c0 >= 0 && c0 < h0 && c1 >= 0 && c1 < w0)) return;
-    const double r0 = L0V(c0, c1);
+    const int c0 = py_index(row), c1 = py_index(col);
     const double dx = (double)p0 - row;
-    double nrow, ncol;
-    if (c0 + 1 >= h0) {
-        nrow = (double)p0 - dx; // IndexError branch (:196-197)
-    } else {
-        const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1; // python index -1 wraps
-        nrow = ((double)p0 - dx) + sub_pix_compute(r0, L0V(c0 + 1, c1), L0V(cm, c1));
+    double nrow = (double)p0 - dx; // the except branch
+    if (py_in(c0 - 1, h0) && py_in(c0 + 1, h0) && py_in(c1, w0)) {
+        const int a = py_wrap(c0, h0), b = py_wrap(c1, w0);
+        nrow = nrow + sub_pix_compute(L0V(a, b), L0V(py_wrap(c0 + 1, h0), b), L0V(py_wrap(c0 - 1, h0), b));
     }
     const double dy = (double)p1 - col;
-    if (c1 + 1 >= w0) {
-        ncol = (double)p1 - dy;
-    } else {
-        const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
-        ncol = ((double)p1 - dy) + sub_pix_compute(r0, L0V(c0, c1 + 1), L0V(c0, cm));
+    double ncol = (double)p1 - dy;
+    if (py_in(c1 - 1, w0) && py_in(c1 + 1, w0) && py_in(c0, h0)) {
+        const int a = py_wrap(c0, h0), b = py_wrap(c1, w0);
+        ncol = ncol + sub_pix_compute(L0V(a, b), L0V(a, py_wrap(c1 + 1, w0)), L0V(a, py_wrap(c1 - 1, w0)));
     }
 #undef L0V
     mt[pc] = nrow;
@@ -1243,6 +1253,33 @@ static bool volume_ls_shape(const dm_tiles *b)   // sizes the workspace: no envi
 }
 
 
+// the row-pair strips of sweep 1 (k_prep_strips): the three GW = 4 instances of the level kernel
+// (packed y, ws <= 5; every wave sweeps 64 windows = 2 strip tiles per row pair)
+#ifndef DM_S1
+#define DM_S1 1   // 0: sweep 1 on the 16 x 16 tiles (A/B build switch)
+#endif
+static bool strip_shape(const dm_tiles *b)   // sizes the workspace: no environment knobs
+{
+    if (!DM_S1 || !mf16_eligible(b) || b->ws > 5) return false;
+    const int G = b->w0 / 16;
+    return G % 4 == 0 && (G / 4 == 1 || G / 4 == 2 || G / 4 == 4);
+}
+
+static size_t strip_bytes(const dm_tiles *b)
+{
+    const size_t rows = (size_t)b->T * (b->h0 / 2);
+    return rows * (b->w0 / 32) * 1024 + rows * b->w0 * 16;
+}
+
+static void strip_views(const dm_tiles *b, void *d_stats, dm_v4i **Bs, dm_v4i **Ss)
+{
+    const size_t extra = mf16_extra_bytes(b);
+    char *base = (char *)d_stats + align256(base_stats_bytes(b)) + align256(extra) +
+                 (volume_ls_shape(b) ? align256(extra) : 0);
+    *Bs = (dm_v4i *)base;
+    *Ss = (dm_v4i *)(base + (size_t)b->T * (b->h0 / 2) * (b->w0 / 32) * 1024);
+}
+
 static void mfma_views2(const dm_tiles *b, void *d_stats, dm_v4i **Bw, int2 **QS)
 {
     const int G = b->w0 / 16;
@@ -1405,7 +1442,7 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 #endif
 template <bool L2F, bool YF>
 static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
-                        hipStream_t st)
+                        hipStream_t st, const dm_v4i *Bs, const dm_v4i *Ss)
 {
     const int KS = (b->ws * b->ws + 63) / 64, NW = mfq_nw(b), GW = b->w0 / 16 / NW;
     const unsigned grid = (unsigned)(b->T * (b->h0 / 4) * (b->w0 / 4));
@@ -1418,7 +1455,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C5_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (Bs) k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        else k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1430,7 +1468,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C2_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (Bs) k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        else k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1440,7 +1479,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C3_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
+        if (Bs) k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        else k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
     }
@@ -1464,8 +1504,10 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
     int2 *QS;
     mfma_views(b, d_stats, &Bw, &QS);
     const Stats s = stats_view(d_stats, b->T, b->h0 * b->w0);
-    if (b->ws <= 5) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st);
-    return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st);
+    dm_v4i *Bs = nullptr, *Ss = nullptr;
+    if (strip_shape(b)) strip_views(b, d_stats, &Bs, &Ss);
+    if (b->ws <= 5) return launch_mfq_t<L2F, true>(b, s, Bw, QS, L1, L2, st, Bs, Ss);
+    return launch_mfq_t<L2F, false>(b, s, Bw, QS, L1, L2, st, nullptr, nullptr);
 }
 
 // LDS-shared-window volume kernel (k_volume_ls): ws <= 5 on the MFMA shapes, 8 waves (patch
@@ -1607,7 +1649,18 @@ static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, O
 
 extern "C" {
 
-int dm_abi_version(void) { return 108; }
+int dm_abi_version(void) { return 109; }
+
+#define DM_STR2(x) #x
+#define DM_STR(x) DM_STR2(x)
+const char *dm_build_config(void)
+{
+    return "S1=" DM_STR(DM_S1) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C5_NB=" DM_STR(DM_C5_NB)
+           " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
+           " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
+           " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_F_NW=" DM_STR(DM_VL_F_NW)
+           " VL_F_TR=" DM_STR(DM_VL_F_TR) " VL_F_MW=" DM_STR(DM_VL_F_MW) " VL_F_NT=" DM_STR(DM_VL_F_NT);
+}
 
 const char *dm_last_error(void) { return g_err; }
 
@@ -1617,8 +1670,11 @@ size_t dm_stats_bytes(const dm_tiles *b)
     size_t n = base_stats_bytes(b), extra = 0;
     if (b->ws >= 1 && b->ws <= 15 && b->T > 0 && b->h0 > 0 && b->w0 > 0 && mf16_eligible(b))
         extra = mf16_extra_bytes(b);
-    if (extra && volume_ls_shape(b)) return align256(n) + align256(extra) + extra;  // + the GW = G region
-    return extra ? align256(n) + extra : n;
+    if (!extra) return n;
+    size_t tot = align256(n) + align256(extra);
+    if (volume_ls_shape(b)) tot += align256(extra);   // + the GW = G region (k_volume_ls)
+    if (strip_shape(b)) tot += strip_bytes(b);        // + the row-pair strips (sweep 1)
+    return tot;
 }
 
 int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
@@ -1641,6 +1697,14 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
         else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
         HIP_TRY(hipGetLastError());
+        if (strip_shape(b)) {
+            dm_v4i *Bs, *Ss;
+            strip_views(b, d_stats, &Bs, &Ss);
+            const size_t ns = (size_t)b->T * (b->h0 / 2) * b->w0;
+            if (b->ws == 5) k_prep_strips<5><<<nblk(ns, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), Bs, Ss);
+            else k_prep_strips<0><<<nblk(ns, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), Bs, Ss);
+            HIP_TRY(hipGetLastError());
+        }
     }
     return DM_OK;
 }
@@ -1948,6 +2012,20 @@ int dm_subpix_map(const double *d_level0, int32_t T, int32_t h0, int32_t w0, int
     const Geo g{};
     const Stats s{};
     k_subpix<<<nblk((size_t)T * hm * wm, 64), 64, 0, (hipStream_t)stream>>>(g, s, d_level0, T, h0, w0, hm, wm, d_map);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_subpix_map_tiles(const dm_tiles *b, const void *d_stats, int32_t hm, int32_t wm, double *d_map, void *stream)
+{
+    int rc = check_tiles(b);
+    if (rc) return rc;
+    if (!d_stats || !d_map) return fail(DM_ERR_ARG, "dm_subpix_map_tiles needs the statistics workspace and the map");
+    if (hm < 1 || wm < 1 || hm > b->h0 || wm > b->w0)
+        return fail(DM_ERR_ARG, "dm_subpix_map_tiles: map %dx%d for level 0 %dx%d", hm, wm, b->h0, b->w0);
+    const Geo g = make_geo(b);
+    const Stats s = stats_view((void *)d_stats, b->T, b->h0 * b->w0);
+    k_subpix<<<nblk((size_t)b->T * hm * wm, 64), 64, 0, (hipStream_t)stream>>>(g, s, nullptr, b->T, b->h0, b->w0, hm, wm, d_map);
     HIP_TRY(hipGetLastError());
     return DM_OK;
 }

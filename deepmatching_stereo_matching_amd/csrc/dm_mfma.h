@@ -101,12 +101,150 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
         }
 }
 
+// ===================================================================================
+// Row-pair strips for v_mfma_i32_32x32x32_i8 (sweep 1 of k_level1_mfq, ws <= 5).
+// The window of (q0, q1) and the one below it, (q0 + 1, q1), lie in one strip of ws + 1 image
+// rows x ws columns, (ws + 1) ws <= 30 taps: strip tap k = ws * row + col (k < 32; the rest
+// zero).  A 32 x 32 i8 MFMA with K = the 32 strip taps then gives 16 patches x 2 window rows
+// x 32 window columns in one instruction: A row i < 16 holds patch i's taps at strip rows
+// 0 .. ws - 1, row 16 + i the same taps one strip row down, so C[i][j] is patch i against
+// window (q0, q1_j) and C[16 + i][j] against (q0 + 1, q1_j).  Four times the products of a
+// 16 x 16 x 32 tile for twice its issue cycles (tools/mfma32_probe.hip).  Operand layout of
+// the gfx950 32x32x32 i8 MFMA: lane L holds row / column L & 31, bytes 16 (L >> 5) .. +15 of
+// K (the same byte order for A and B, which is all a dot product needs); result register r
+// of lane L is C[8 (r >> 2) + 4 (L >> 5) + (r & 3)][L & 31].
+//   Bs[t][rp][q1 / 32][lane]  16 B: strip taps 16 (lane >> 5) .. +15 of window column
+//                             q1 = 32 (q1 / 32) + (lane & 31), rows q0 = 2 rp .. q0 + ws
+//   Ss[t][rp][q1]             {qx, qy} of window (q0, q1), then of (q0 + 1, q1) -- the same
+//                             bits as QS16's (k_prep_windows16)
+// ===================================================================================
+typedef int dm_v16i __attribute__((ext_vector_type(16)));
+typedef float dm_f2 __attribute__((ext_vector_type(2)));
+
+// {bits(f32(-sum I')), bits(b_q)} of a window from its taps (k_prep_windows16's arithmetic)
+__device__ __forceinline__ int2 window_qs(int s, int s2, int n, int method)
+{
+    const long long dI = (long long)n * s2 - (long long)s * s;
+    float bq;
+    if (method == DM_TM_CCOEFF) bq = 1.0f;
+    else bq = dI == 0 ? 0.0f : (float)(1.0 / sqrt((double)dI));
+    return make_int2(__float_as_int((float)-s), __float_as_int(bq));
+}
+
+// buffer resource over a tile's image crop (origin of tile t, wave-uniform t): scalar, so the
+// byte loads through it need no per-lane resource (no waterfall loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t *img, int pitch, const Geo &g, int t)
+{
+    const int ro = __builtin_amdgcn_readfirstlane(g.org[2 * t]), co = __builtin_amdgcn_readfirstlane(g.org[2 * t + 1]);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(img + (size_t)ro * pitch + co), 0, 0x7fffffff, 0x00020000);
+}
+
+// WSC: ws known at compile time (5), 0 = g.ws (<= 5)
+template <int WSC>
+__global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
+{
+    DM_TAIL_ENTRY();
+    const int ws = WSC ? WSC : g.ws, NS = (ws + 1) * ws;
+    const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const int h2 = g.h0 / 2, w0 = g.w0;
+    if (idx >= (size_t)g.T * h2 * w0) return;
+    const int q1 = (int)(idx % w0);
+    const int rp = (int)((idx / w0) % h2);
+    const int t = (int)(idx / ((size_t)w0 * h2));
+    const uint8_t *base = g.img2 + (size_t)(g.org[2 * t] + 2 * rp) * g.pitch2 + g.org[2 * t + 1] + q1;
+    int pix[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) pix[k] = k < NS ? (int)base[(size_t)(k / ws) * g.pitch2 + (k % ws)] - 128 : 0;
+    int2 qs[2];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        int s = 0, s2 = 0;
+#pragma unroll
+        for (int k = 0; k < 30; ++k) {
+            if (k >= ws * ws) break;
+            const int v = pix[o * ws + k];
+            s += v; s2 += v * v;
+        }
+        qs[o] = window_qs(s, s2, ws * ws, g.method);
+    }
+    Ss[idx] = dm_v4i{qs[0].x, qs[0].y, qs[1].x, qs[1].y};
+    const size_t tile = idx / 32; // (t, rp, q1 / 32): w0 % 32 == 0
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        int w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j >> 2] |= (pix[16 * h + j] & 0xFF) << (8 * (j & 3));
+        Bs[tile * 64 + (q1 % 32) + 32 * h] = dm_v4i{w[0], w[1], w[2], w[3]};
+    }
+}
+
+// A operand of the strip MFMA: lane L, row i = L & 31 = patch i & 15 of the 2 x 2 cell block
+// (cell (i & 15) >> 2, child i & 3, as build_a's row c) at strip offset i >> 4
+// (WSC: ws known at compile time -- the byte loads unrolled and issued together; 0 = g.ws)
+template <int WSC>
+__device__ __forceinline__ dm_v4i build_a_strip(const Geo &g, int t, int I0, int J0, int lane)
+{
+    const int ws = WSC ? WSC : g.ws, NS = (ws + 1) * ws;
+    const int i = lane & 31, h = lane >> 5, pi = i & 15, o = i >> 4;
+    const int cl = pi >> 2, ch = pi & 3;
+    const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+    // byte loads at 32-bit offsets from the tile's origin (one uniform buffer resource), every
+    // byte from a clamped in-patch address and then kept or zeroed: no 64-bit address per
+    // byte, no branch, the 16 loads in flight together
+    const __amdgpu_buffer_rsrc_t rI = tile_rsrc(g.img1, g.pitch1, g, t);
+    const unsigned pb = (unsigned)(p0 * g.pitch1 + p1);
+    int w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int k = 16 * h + j;
+        const int row = k / ws - o, col = k % ws;
+        const bool in = k < NS && row >= 0 && row < ws;
+        const int rc = row < 0 ? 0 : (row >= ws ? ws - 1 : row);
+        const int v = (int)__builtin_amdgcn_raw_buffer_load_b8(rI, pb + (unsigned)(rc * g.pitch1 + (k < NS ? col : 0)), 0, 0) - 128;
+        w[j >> 2] |= ((in ? v : 0) & 0xFF) << (8 * (j & 3));
+    }
+    return dm_v4i{w[0], w[1], w[2], w[3]};
+}
+
+// min of mn[k] / max of mx[k] over the 32 lanes of each half-wave by DPP: row rotations 8, 4, 2,
+// 1 leave every lane of a 16-lane row with the row's extreme, then row_bcast:15 folds row 0 into
+// row 1 and row 2 into row 3 -- lanes 31 and 63 hold the two halves' results.  Each step is one
+// VOP2-DPP instruction (v = op(dpp(v), v), vdst tied to v: rows the row_mask excludes keep it),
+// issued for all 2N values before the next step, so no instruction reads a VGPR the one just
+// before it wrote (the DPP read-after-VALU-write hazard needs 2 wait states); the values are
+// never NaN.  (Five DPP instructions per value instead of five ds_bpermute shuffles.)
+template <int N>
+__device__ __forceinline__ void half_wave_minmax(float (&mn)[N], float (&mx)[N])
+{
+    static_assert(N >= 1, "");
+#define DM_HWR(ctl, rm)                                                                                   \
+    _Pragma("unroll") for (int k = 0; k < N; ++k) {                                                       \
+        asm volatile("v_min_f32_dpp %0, %0, %0 " ctl " row_mask:" rm " bank_mask:0xf" : "+v"(mn[k]));      \
+        asm volatile("v_max_f32_dpp %0, %0, %0 " ctl " row_mask:" rm " bank_mask:0xf" : "+v"(mx[k]));      \
+    }
+    asm volatile("s_nop 1" ::: "memory"); // the values' last VALU writes may be just before
+    DM_HWR("row_ror:8", "0xf")
+    DM_HWR("row_ror:4", "0xf")
+    DM_HWR("row_ror:2", "0xf")
+    DM_HWR("row_ror:1", "0xf")
+    DM_HWR("row_bcast:15", "0xa")
+#undef DM_HWR
+}
+
+// {q.y, q.y} * v as one v_pk_mul_f32 (op_sel broadcast of the high half: the compiler would
+// copy q.y into an even register first)
+__device__ __forceinline__ dm_f2 pk_mul_bhi(dm_f2 q, dm_f2 v)
+{
+    dm_f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(q), "v"(v));
+    return r;
+}
+
 // Window stats of this lane's window from its own B fragment (spread layout: KS == 1,
 // n <= 32, i8): words 2, 3 = {qx, qy}, qx = f32 bits of -sum(I'), qy = b_q of window c --
 // an aligned register pair whose halves the packed y arithmetic broadcasts with op_sel.
 // (Round 2 first carried them in lanes 32..63 only and moved them with two
 // v_permlane32_swap per tile: 8 issue cycles each on gfx950, tools/valu_probe.hip.)
-typedef float dm_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ dm_f2 qs_of_frag(const dm_v4i &b)
 {
     return dm_f2{__int_as_float(b.z), __int_as_float(b.w)};
@@ -162,14 +300,15 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
     if constexpr (YF) {
         const float nf = (float)n;
         const float nb = -nf * 12582912.0f;   // exact (see above)
-        const dm_f2 sI2 = __builtin_shufflevector(q2, q2, 0, 0), b2 = __builtin_shufflevector(q2, q2, 1, 1);
+        const dm_f2 sI2 = __builtin_shufflevector(q2, q2, 0, 0);
         const dm_f2 a01 = dm_f2{__int_as_float(acc[0]), __int_as_float(acc[1])};
         const dm_f2 a23 = dm_f2{__int_as_float(acc[2]), __int_as_float(acc[3])};
         const dm_f2 m01 = __builtin_elementwise_fma(a01, dm_f2{nf, nf}, dm_f2{nb, nb});
         const dm_f2 m23 = __builtin_elementwise_fma(a23, dm_f2{nf, nf}, dm_f2{nb, nb});
         const dm_f2 n01 = __builtin_elementwise_fma(dm_f2{sTf[0], sTf[1]}, sI2, m01);
         const dm_f2 n23 = __builtin_elementwise_fma(dm_f2{sTf[2], sTf[3]}, sI2, m23);
-        const dm_f2 y01 = n01 * b2, y23 = n23 * b2;
+        // b_q broadcast from the pair's high half by op_sel (no copy into an even register)
+        const dm_f2 y01 = pk_mul_bhi(q2, n01), y23 = pk_mul_bhi(q2, n23);
         y[0] = y01.x; y[1] = y01.y; y[2] = y23.x; y[3] = y23.y;
     } else {
         const float b = q2.y;
@@ -181,10 +320,12 @@ __device__ __forceinline__ void y_of_acc(const dm_v4i &acc, const int *sTr, cons
 
 // A operand of one lane: patch rows of a 2x2 cell block (row c: cell cl = c/4, child ch = c%4),
 // int8 taps 64ks + 16grp + j (spread layout, KS == 1 and n <= 32: taps 8grp + j)
-template <int KS>
+// (WSC: ws known at compile time, 0 = g.ws; spread layout: branch-free byte loads from clamped
+// in-patch addresses, so they issue together)
+template <int KS, int WSC = 0>
 __device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, int J0, int c, int grp)
 {
-    const int n = g.ws * g.ws;
+    const int ws = WSC ? WSC : g.ws, n = ws * ws;
     const int cl = c >> 2, ch = c & 3;
     const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
     const uint8_t *base = g.img1 + (size_t)(g.org[2 * t] + p0) * g.pitch1 + g.org[2 * t + 1] + p1;
@@ -192,11 +333,13 @@ __device__ __forceinline__ void build_a(dm_v4i *A, const Geo &g, int t, int I0, 
     for (int ks = 0; ks < KS; ++ks) {
         int w[4] = {0, 0, 0, 0};
         if (KS == 1 && n <= 32) { // spread layout (k_prep_windows16): taps 8 grp + j
+            const __amdgpu_buffer_rsrc_t rI = tile_rsrc(g.img1, g.pitch1, g, t);
+            const unsigned pb = (unsigned)(p0 * g.pitch1 + p1);
+#pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int k = 8 * grp + j;
-                int val = 0;
-                if (k < n) val = (int)base[(size_t)(k / g.ws) * g.pitch1 + (k % g.ws)] - 128;
-                w[j >> 2] |= (val & 0xFF) << (8 * (j & 3));
+                const int k = 8 * grp + j, kc = k < n ? k : n - 1;
+                const int v = (int)__builtin_amdgcn_raw_buffer_load_b8(rI, pb + (unsigned)((kc / ws) * g.pitch1 + (kc % ws)), 0, 0) - 128;
+                w[j >> 2] |= ((k < n ? v : 0) & 0xFF) << (8 * (j & 3));
             }
         } else {
             for (int j = 0; j < 16; ++j) {
@@ -329,9 +472,14 @@ struct XchOwn<true, T, OFF> {
 // NB 2x2-cell blocks per workgroup (NB = 2 where one wave spans a whole tile row, S = 64):
 // waves sb * NWc .. sb * NWc + NWc - 1 split block sb's columns; the blocks share the pow
 // tables, which is what a workgroup of more than one wave buys there.
-template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, int NB = 1, bool CL = false>
+// S1: sweep 1 on the row-pair strips (Bs, Ss: k_prep_strips) with the 32 x 32 x 32 i8 MFMA --
+// half the matrix-core issue cycles of the 16 x 16 tiles per voxel, and the window stats
+// broadcast without copies; sweep 2 keeps the 16 x 16 layout its pooling needs.
+template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, int NB = 1, bool CL = false, bool S1 = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                        const int2 *__restrict__ QS, double *L1, double *L2)
+                                                        const int2 *__restrict__ QS, double *L1, double *L2,
+                                                        const dm_v4i *__restrict__ Bs = nullptr,
+                                                        const dm_v4i *__restrict__ Ss = nullptr)
 {
     constexpr bool EQ = KS == 1 && YF;           // window stats ride in the B tile (qs_of_frag)
     static_assert(NW % NB == 0, "blocks split the waves evenly");
@@ -393,16 +541,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     const int ro = g.org[2 * t], co = g.org[2 * t + 1];
 
     dm_v4i A[KS];
-    build_a<KS>(A, g, t, I0, J0, c, grp);
     const int Ic = I0 + (grp >> 1), Jc = J0 + (grp & 1);
     int sTr[4];
     float sTf[4];
+    // the 16 x 16 tiles' patch operand and sums (S1: built after the strip sweep, which does
+    // not read them -- they would hold registers through it)
+    auto init_a16 = [&]() {
+        if (g.ws == 5) build_a<KS, 5>(A, g, t, I0, J0, c, grp);
+        else build_a<KS>(A, g, t, I0, J0, c, grp);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
-        sTr[r] = s.sT[tb + p];
-        sTf[r] = (float)sTr[r];
-    }
+        for (int r = 0; r < 4; ++r) {
+            const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
+            sTr[r] = s.sT[tb + p];
+            sTf[r] = (float)sTr[r];
+        }
+    };
+    if constexpr (!S1) init_a16();
     const int ab = YF ? DM_YBIAS : 0;
     const dm_v4i acc0 = {ab, ab, ab, ab};
     const unsigned mant = mant_mask_vgpr();   // pow14_zf's mantissa mask, kept in a VGPR
@@ -453,6 +607,83 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         }
     };
     RowFrag fa, fb;
+    if constexpr (S1) {
+        static_assert(YF && KS == 1 && GW == 4, "strip sweep: packed y, one 64-window column group per wave");
+        // this wave's windows: strip tiles 2 wc, 2 wc + 1 (32 columns each) of every row pair;
+        // lane (c32, hs) holds cells hs, 2 + hs of the block at window column c32, both rows
+        const int c32 = lane & 31, hs = lane >> 5;
+        const dm_v4i A32 = g.ws == 5 ? build_a_strip<5>(g, t, I0, J0, lane) : build_a_strip<0>(g, t, I0, J0, lane);
+        float sTs[8]; // [cell slot cs][child]: cell 2 cs + hs
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int cell = 2 * (k >> 2) + hs, ch = k & 3;
+            const int p = (2 * (I0 + (cell >> 1)) + (ch >> 1)) * w0 + 2 * (J0 + (cell & 1)) + (ch & 1);
+            sTs[k] = (float)s.sT[tb + p];
+        }
+        float mn8[8], mx8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { mn8[k] = INFINITY; mx8[k] = -INFINITY; }
+        const int h2 = h0 / 2, NT32 = w0 / 32;
+        const __amdgpu_buffer_rsrc_t rS1 = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Bs + ((size_t)t * h2 * NT32 + 2 * wc) * 64), 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rS2 = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Ss + (size_t)t * h2 * w0 + 64 * wc), 0, 0x7fffffff, 0x00020000);
+        const unsigned voS = (unsigned)lane * 16u, voQ2 = (unsigned)c32 * 16u;
+        struct StripFrag {
+            dm_v4i b[2], q[2];
+        };
+        auto load_strip = [&](StripFrag &f, int rp) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)(rp * NT32 + j) * 1024u, 0);
+                f.q[j] = __builtin_amdgcn_raw_buffer_load_b128(rS2, voQ2, (unsigned)(rp * w0 + 32 * j) * 16u, 0);
+            }
+        };
+        const float nf = (float)n, nb = -nf * 12582912.0f; // y_of_acc's exact steps
+        const dm_v16i acc32 = {DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS,
+                               DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS};
+        auto minmax_strip = [&](const StripFrag &f) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const dm_v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A32, f.b[j], acc32, 0, 0, 0);
+                const dm_f2 qs0 = dm_f2{__int_as_float(f.q[j].x), __int_as_float(f.q[j].y)};
+                const dm_f2 qs1 = dm_f2{__int_as_float(f.q[j].z), __int_as_float(f.q[j].w)};
+                float y[16];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) { // register pair (2m, 2m + 1): row 8 (m >> 2) + 4 hs + 2 (m & 1) + {0, 1}
+                    const int q = m >> 1, cs = q & 1, cp = m & 1;
+                    const dm_f2 qs = (q >> 1) ? qs1 : qs0;  // window row q0 + (q >> 1)
+                    const dm_f2 a = dm_f2{__int_as_float(acc[2 * m]), __int_as_float(acc[2 * m + 1])};
+                    const dm_f2 mm = __builtin_elementwise_fma(a, dm_f2{nf, nf}, dm_f2{nb, nb});
+                    const dm_f2 nu = __builtin_elementwise_fma(dm_f2{sTs[4 * cs + 2 * cp], sTs[4 * cs + 2 * cp + 1]},
+                                                               __builtin_shufflevector(qs, qs, 0, 0), mm);
+                    const dm_f2 yy = pk_mul_bhi(qs, nu);
+                    y[2 * m] = yy.x; y[2 * m + 1] = yy.y;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { // (cs, child): rows q0 (register k) and q0 + 1 (8 + k)
+                    mn8[k] = fminf(fminf(mn8[k], y[k]), y[8 + k]);
+                    mx8[k] = fmaxf(fmaxf(mx8[k], y[k]), y[8 + k]);
+                }
+            }
+        };
+        StripFrag sa, sb2;
+        load_strip(sa, 0);
+        for (int rp = 0; rp < h2; rp += 2) { // h2 even (h0 % 4 == 0)
+            load_strip(sb2, rp + 1);
+            minmax_strip(sa);
+            load_strip(sa, rp + 2 < h2 ? rp + 2 : rp); // (the last one: in range, unused)
+            minmax_strip(sb2);
+        }
+        load_row(fa, 0); // sweep 2's first row, in flight through the reduction
+        init_a16();
+        half_wave_minmax(mn8, mx8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int pl = 4 * (2 * (k >> 2) + hs) + (k & 3);  // patch row of the block: 4 cell + child
+            if (c32 == 31) { red[sb][0][wc][pl] = mn8[k]; red[sb][1][wc][pl] = mx8[k]; }
+        }
+    } else {
     load_row(fa, 0);
     for (int q0 = 0; q0 < h0; q0 += 2) { // h0 % 4 == 0
         load_row(fb, q0 + 1);
@@ -467,6 +698,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
         }
         if (c == 0) { red[sb][0][wc][4 * grp + r] = mn[r]; red[sb][1][wc][4 * grp + r] = mx[r]; }
+    }
     }
     __syncthreads();
     // per-patch normalisation constants {a_p, rmin, rmax - rmin, RN(1/(rmax - rmin))} of the

@@ -380,20 +380,43 @@ def match_levels(levels, sub_pix=True, filtering=False, filter_window_size=3, fi
 def subpix_map(level0, match):
     """Matching._sub_pix_cal (Matching.py:177-209) in place on a map that a descent left at a
     level above 0: `match` float64 [3][hm][wm] (device), refined against co_map_list[0]
-    (`level0`: [h0][w0][h0][w0] or [h0*w0][h0*w0], host or device) at patch (i, j) and window
-    (row, col) of each entry, as the reference does (dm_subpix_map)."""
+    (`level0`: [h0][w0][h0][w0], host or device) at patch (i, j) and window (row, col) of each
+    entry, as the reference does (dm_subpix_map).  Any entry is accepted and indexed the way
+    numpy indexes co_map_list[0] (negative indices wrap, out-of-range ones take the
+    reference's except branch)."""
     lib = L.load()
+    if not isinstance(match, torch.Tensor) or not match.is_cuda:
+        raise ValueError('match must be a device (cuda) tensor: the kernel refines it in place')
+    if not match.is_contiguous() or match.dtype != torch.float64 or match.dim() != 3 or match.shape[0] != 3:
+        raise ValueError('match must be a contiguous float64 [3][h][w] tensor')
     dev = match.device
     l0 = torch.as_tensor(level0, dtype=torch.float64).to(dev).contiguous()
-    if l0.dim() == 4:
-        h0, w0 = l0.shape[:2]
-    else:
+    if l0.dim() != 4:
         raise ValueError('level 0 must be [h0][w0][h0][w0]')
+    h0, w0 = l0.shape[:2]
     _, hm, wm = match.shape
-    if not match.is_contiguous() or match.dtype != torch.float64:
-        raise ValueError('match must be a contiguous float64 [3][h][w] tensor')
     L.check(lib.dm_subpix_map(L.ptr(l0), 1, h0, w0, hm, wm, L.ptr(match), L.stream_handle()),
             'dm_subpix_map')
+    return match
+
+
+def subpix_map_tiles(pyr, match, stream=None):
+    """subpix_map with level 0 on demand (dm_subpix_map_tiles): the five level-0 values an entry
+    reads are recomputed from the pyramid's images and statistics, so co_map_list[0] is never
+    materialised.  `match`: contiguous float64 device tensor [T][3][hm][wm] (or [3][hm][wm]
+    when the batch holds one tile), refined in place."""
+    if not isinstance(match, torch.Tensor) or not match.is_cuda:
+        raise ValueError('match must be a device (cuda) tensor: the kernel refines it in place')
+    m = match if match.dim() == 4 else match[None]
+    b = pyr.b
+    if not m.is_contiguous() or m.dtype != torch.float64 or m.shape[0] != b.T or m.shape[1] != 3:
+        raise ValueError('match must be a contiguous float64 [T][3][h][w] tensor (T = %d)' % b.T)
+    if not pyr._have_minmax:   # the per-patch min / max a level kernel or volume leaves in the stats
+        pyr.build(nlev=2)
+    _, _, hm, wm = m.shape
+    L.check(pyr.lib.dm_subpix_map_tiles(b.ref(), L.ptr(pyr.stats), hm, wm, L.ptr(m),
+                                        L.stream_handle(stream) if stream is not None else pyr._s()),
+            'dm_subpix_map_tiles')
     return match
 
 

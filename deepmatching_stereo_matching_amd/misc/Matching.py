@@ -89,7 +89,8 @@ class Matching():
         fnum = self.filtering_num if self.filtering else 0
         # a descent that stops above level 0 is refined against co_map_list[0] all the same,
         # at the coarse map's (i, j, row, col) (:182-186): match without sub-pixel, then
-        # dm_subpix_map on level 0
+        # dm_subpix_map_tiles (level 0 on demand from the images, never materialised) or, for
+        # a plain co_map_list, dm_subpix_map on the given level 0
         sub_here = self.sub_pix and bottom == 0
         pyr = getattr(lst, 'pyramid', None)
         if isinstance(pyr, engine.DevicePyramid) and bottom == 0:
@@ -103,9 +104,10 @@ class Matching():
             out = engine.match_levels([lst[k] for k in range(bottom, n)], sub_here, self.filtering,
                                       self.filter_window_size, fnum, self.filtering_mode)
         if self.sub_pix and bottom > 0:
-            l0 = lst.device(0).reshape(pyr.level_shape(0)) if isinstance(pyr, engine.DevicePyramid) \
-                else lst[0]
-            engine.subpix_map(l0, out)
+            if isinstance(pyr, engine.DevicePyramid):
+                engine.subpix_map_tiles(pyr, out)
+            else:
+                engine.subpix_map(lst[0], out)
         if self.filtering:  # _initial_move_map / _B decrement it once per level (:91-93, :136-138)
             self.filtering_num = max(0, self.filtering_num - (steps + 1))
         return out

@@ -177,10 +177,21 @@ int dm_match(const dm_tiles *b, const void *d_stats, const double *const *d_leve
  * map of a coarser level (float64 [T][3][hm][wm], from dm_match on co_map_list[bottom:]
  * without sub_pix) is refined in place against the materialised level 0 d_level0 (float64
  * [T][h0*w0][h0*w0], co_map_list[0]) at patch (i, j) and window (row, col) of each entry, as
- * the reference does; bounds are level 0's (h0, w0), index -1 wraps as in Python.  hm <= h0,
- * wm <= w0.  dm_match's own sub_pix is this with hm = h0, wm = w0. */
+ * the reference does; bounds are level 0's (h0, w0).  Any map is accepted and indexed as numpy
+ * indexes co_map_list[0] (Matching.py:186-188, :199-201): c = int(entry), an index in [-N, N)
+ * is valid and a negative one wraps, any other raises IndexError and takes the bare except
+ * (:193-194, :205-206: i - d_x, j - d_y).  hm <= h0, wm <= w0.  dm_match's own sub_pix is
+ * this with hm = h0, wm = w0. */
 int dm_subpix_map(const double *d_level0, int32_t T, int32_t h0, int32_t w0, int32_t hm, int32_t wm,
                   double *d_map, void *stream);
+
+/* The same refinement with level 0 evaluated on demand (ABI 1.9): the five level-0 values an
+ * entry reads are recomputed from the tile batch's images and the statistics workspace of
+ * dm_corr_stats + dm_corr_level1/12 (its per-patch min / max), exactly as dm_match's own
+ * sub-pixel step does, so a descent that stops above level 0 never materialises
+ * co_map_list[0] (T * (h0 w0)^2 float64).  d_map: float64 [b->T][3][hm][wm], in place. */
+int dm_subpix_map_tiles(const dm_tiles *b, const void *d_stats, int32_t hm, int32_t wm, double *d_map,
+                        void *stream);
 
 /* misc/sub_pix_cal.py sub_pix_cal (:22-53): clamp to [-3,3], quadratic refinement of an
  * (h, w) disparity map along `direction` (0 rows, 1 cols) on the score map scaled by
@@ -266,15 +277,21 @@ int dm_opt_loop_bilateral(double *d_img, const double *d_color, const double *d_
  * error sums. */
 int dm_seq_sum(const double *d_v, int64_t n, double *d_out, void *stream);
 
+/* The compile-time kernel switches this library was built with ("S1=1 C2_NB=4 ..."; see
+ * dm_kernels.hip: DM_S1, DM_C*_NB, DM_VL_*), which decide the kernel instance each shape
+ * launches -- tools/kernel_hash.py derives the profiled instances' symbols from it. */
+const char *dm_build_config(void);
+
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 108 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 109 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
  * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
  * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum,
- * 1.8 dm_subpix_map). */
+ * 1.8 dm_subpix_map, 1.9 dm_subpix_map_tiles and the row-pair strips of dm_corr_stats'
+ * workspace for the level kernel's min / max sweep). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

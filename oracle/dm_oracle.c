@@ -357,29 +357,36 @@ static double sub_pix_compute(double r0, double r1, double r_)
 }
 
 /* Matching._sub_pix_cal for one pixel (misc/Matching.py:177-209) on its rectified level-0
- * map M (h0 x w0): rows, then columns; index -1 wraps (python), index h0 / w0 raises
- * IndexError -> bare except -> no change. */
+ * map M (h0 x w0): rows, then columns.  c = int(entry) indexes co_map_list[0][i, j] the numpy
+ * way: an index in [-N, N) is valid and a negative one wraps, any other raises IndexError ->
+ * bare except -> i - d_x (j - d_y).  The row step reads (c0 - 1 | c0 | c0 + 1, c1), the
+ * column step (c0, c1 - 1 | c1 | c1 + 1).  (NaN / huge entries: the reference's int() raises
+ * outside the try; taken as the except branch here.) */
+static int py_index(double v) { return (v == v && fabs(v) < 1073741824.0) ? (int)v : -0x40000000; }
+static int py_in(int k, int n) { return k >= -n && k < n; }
+static int py_wrap(int k, int n) { return k < 0 ? k + n : k; }
+
 static void sub_pix_one(const double *M, int h0, int w0, int i, int j, double *m0, double *m1)
 {
-    const int c0 = (int)*m0, c1 = (int)*m1;
+    const int c0 = py_index(*m0), c1 = py_index(*m1);
     const double d_x = i - *m0;
-    if (c0 + 1 >= h0) {
-        *m0 = i - d_x;                                   /* IndexError branch */
-    } else {
-        const int cm = c0 - 1 < 0 ? h0 - 1 : c0 - 1;     /* python wraps -1 */
-        const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)(c0 + 1) * w0 + c1],
-                     r_ = M[(long)cm * w0 + c1];
-        *m0 = i - d_x + sub_pix_compute(r0, r1, r_);
+    double v = i - d_x;                                  /* IndexError branch */
+    if (py_in(c0 - 1, h0) && py_in(c0 + 1, h0) && py_in(c1, w0)) {
+        const long b = py_wrap(c1, w0);
+        const double r0 = M[(long)py_wrap(c0, h0) * w0 + b], r1 = M[(long)py_wrap(c0 + 1, h0) * w0 + b],
+                     r_ = M[(long)py_wrap(c0 - 1, h0) * w0 + b];
+        v = v + sub_pix_compute(r0, r1, r_);
     }
+    *m0 = v;
     const double d_y = j - *m1;
-    if (c1 + 1 >= w0) {
-        *m1 = j - d_y;
-    } else {
-        const int cm = c1 - 1 < 0 ? w0 - 1 : c1 - 1;
-        const double r0 = M[(long)c0 * w0 + c1], r1 = M[(long)c0 * w0 + c1 + 1],
-                     r_ = M[(long)c0 * w0 + cm];
-        *m1 = j - d_y + sub_pix_compute(r0, r1, r_);
+    v = j - d_y;
+    if (py_in(c1 - 1, w0) && py_in(c1 + 1, w0) && py_in(c0, h0)) {
+        const long a = (long)py_wrap(c0, h0) * w0;
+        const double r0 = M[a + py_wrap(c1, w0)], r1 = M[a + py_wrap(c1 + 1, w0)],
+                     r_ = M[a + py_wrap(c1 - 1, w0)];
+        v = v + sub_pix_compute(r0, r1, r_);
     }
+    *m1 = v;
 }
 
 static const int OFF[4][2] = {{1, 1}, {0, 1}, {1, 0}, {0, 0}};   /* _B's o order (:111) */

@@ -331,28 +331,38 @@ def _match_filtered(levels, sub_pix, fw, fnum, fmode):
     return mp
 
 
+def _py_index(v):
+    """int(v) as the reference's list comprehension takes it (Matching.py:183); None where int()
+    would raise (NaN) or the index cannot be in range."""
+    if v != v or abs(v) >= 2 ** 30:
+        return None
+    return int(v)
+
+
 def _sub_pix(mp, L0):
     """Matching._sub_pix_cal (Matching.py:177-209): the map may be a coarser level's (a
     descent that stops above level 0); co_map_list[0] is read at (i, j, row, col) of each
-    entry and the bounds are level 0's window sides."""
+    entry and the bounds are level 0's window sides.  Indices behave as numpy's on
+    co_map_list[0][i, j] (wrap in [-N, 0), IndexError outside [-N, N) -> the bare except)."""
     def comp(r0, r1, r_):
         return -(r1 - r_) / (2 * (r1 + r_ - 2 * r0)) if (r0 > r1 and r0 > r_) else 0
+
+    def ok(k, n):
+        return k is not None and -n <= k < n
     h0, w0 = L0.shape[2:]
     for i in range(mp.shape[1]):
         for j in range(mp.shape[2]):
-            c0, c1 = int(mp[0, i, j]), int(mp[1, i, j])
+            c0, c1 = _py_index(mp[0, i, j]), _py_index(mp[1, i, j])
             d_x = i - mp[0, i, j]
-            if c0 + 1 >= h0:
+            if ok(c0, h0) and ok(c0 + 1, h0) and ok(c0 - 1, h0) and ok(c1, w0):
+                mp[0, i, j] = i - d_x + comp(L0[i, j, c0, c1], L0[i, j, c0 + 1, c1], L0[i, j, c0 - 1, c1])
+            else:
                 mp[0, i, j] = i - d_x
-            else:
-                mp[0, i, j] = i - d_x + comp(L0[i, j, c0, c1], L0[i, j, c0 + 1, c1],
-                                             L0[i, j, c0 - 1, c1])
             d_y = j - mp[1, i, j]
-            if c1 + 1 >= w0:
-                mp[1, i, j] = j - d_y
+            if ok(c0, h0) and ok(c1, w0) and ok(c1 + 1, w0) and ok(c1 - 1, w0):
+                mp[1, i, j] = j - d_y + comp(L0[i, j, c0, c1], L0[i, j, c0, c1 + 1], L0[i, j, c0, c1 - 1])
             else:
-                mp[1, i, j] = j - d_y + comp(L0[i, j, c0, c1], L0[i, j, c0, c1 + 1],
-                                             L0[i, j, c0, c1 - 1])
+                mp[1, i, j] = j - d_y
     return mp
 
 

@@ -4,9 +4,9 @@
 The reference (misc/Matching.py:85-96, :133-134) descends one level per halving of N_map, so
 an N_map smaller than 2^(n-1) leaves the final map at level `bottom` > 0; _sub_pix_cal
 (:177-209) then still reads co_map_list[0] at (i, j, row, col) of that coarse map.
-tests/golden/stop_above_l0_s{16,32}.npz hold the reference's own outputs for bottom = 1, 2
-(tests/golden/make_golden_r04.py).  CPU: the oracle (oracle.match_from) against them.  GPU:
-the mirror's Matching (engine.match_levels + dm_subpix_map) against them and, bit for bit,
+tests/golden/stop_above_l0_s{16,32}.npz (tests/golden/make_golden_r04.py) and
+stop_above_l0_s64.npz (make_golden_r05.py) hold the reference's own outputs for bottom = 1, 2.  CPU: the oracle (oracle.match_from) against them.  GPU:
+the mirror's Matching (engine.match_levels + dm_subpix_map_tiles, level 0 on demand) against them and, bit for bit,
 against the oracle on the same levels.
 
 Tolerances as tests/test_oracle_golden.py: integer correspondences exact; scores |d| <= 1e-12;
@@ -21,7 +21,7 @@ from oracle import oracle as O
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 TOL_F64 = 1e-12
 TOL_SUBPIX = 1e-9
-NAMES = ['stop_above_l0_s16', 'stop_above_l0_s32']
+NAMES = ['stop_above_l0_s16', 'stop_above_l0_s32', 'stop_above_l0_s64']
 
 
 def _close(a, b, tol):

@@ -12,6 +12,7 @@
 #           plain (p) stores (DM_VL_H_*; results exact); h2w8 / h2w2: 8 / 2 waves per workgroup (4 in-tree)
 #   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
+#   s0      sweep 1 on the 16 x 16 tiles instead of the row-pair strips (DM_S1=0; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
 #   c5h2w4, c5f4m   the w0 = 256 volumes: binary16 min/max known with 2 x 512-B runs in
@@ -91,6 +92,7 @@ PY
     c3nb1) EXTRA="-DDM_C3_NB=1" ;;
     c5nb2) EXTRA="-DDM_C5_NB=2" ;;
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
+    s0) EXTRA="-DDM_S1=0" ;;
     head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
           (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
              case $f in include/*) git show HEAD:$f > $r/$f ;; *) git show HEAD:$f > $d/csrc/$(basename $f) ;; esac; done) ;;

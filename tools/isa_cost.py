@@ -15,6 +15,9 @@ instruction on one SIMD, many waves):
        independent VALU work on its SIMD (profiles/r03_valu_probe.txt: one MFMA + N v_fma_f32 per
        step takes ~13.4 + 2.4 N cycles for K=64 and ~11.2 + 2.2 N for K=32, N = 4..12; both take
        16 cycles alone)
+  22   v_mfma_i32_32x32x32_i8 (the row-pair strips of sweep 1, round 5): 41.6 cycles with 8
+       v_fma_f32 and 56.1 with 16 in the same probe, i.e. 24.0 / 20.9 besides their 2.2 each
+       (35.9 alone)
 
 and, given per-block execution counts per wave (--weights file: {"block": count}), the
 modelled issue cycles per wave.  Without weights it prints the per-block table, which is
@@ -35,6 +38,8 @@ TRANS = re.compile(r'^v_(exp|log|rcp|rsq|sqrt|sin|cos)_f32|^v_permlane32_swap')
 
 def cost(op, line):
     if op.startswith('v_mfma'):
+        if '32x32x32' in op:
+            return 22.0
         return 11.2 if '16x16x32' in op else 14.0
     if TRANS.match(op):
         return 8.0

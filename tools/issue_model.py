@@ -24,11 +24,11 @@ import isa_cost  # noqa: E402
 import kernel_hash  # noqa: E402
 
 KERNELS = {  # shape -> (kernel symbol substring, weights file, pmc file, waves per launch)
-    'c3': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE', 'issue_model_level1_c3_weights.json',
+    'c3': (kernel_hash.symbol('level', 128), 'issue_model_level1_c3_weights.json',
            'pmc_level1.json', 64 * (128 // 4) * (128 // 4) * 2),
-    'c2': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE', 'issue_model_level1_c2_weights.json',
+    'c2': (kernel_hash.symbol('level', 64), 'issue_model_level1_c2_weights.json',
            'pmc_level1_s64.json', 64 * (64 // 4) * (64 // 4)),
-    'c5': ('k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE', 'issue_model_level1_c5_weights.json',
+    'c5': (kernel_hash.symbol('level', 256), 'issue_model_level1_c5_weights.json',
            'pmc_level1_s256.json', 256 * (256 // 4) * (256 // 4) * 4),
 }
 

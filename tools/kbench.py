@@ -25,6 +25,7 @@ def main():
     ap.add_argument('--tile', type=int, default=128)
     ap.add_argument('--grid', type=int, default=8)
     ap.add_argument('--ws', type=int, default=5)
+    ap.add_argument('--sha', action='store_true', help='print the sha256 of the whole first output')
     args = ap.parse_args()
     S, ws = args.tile, args.ws
     side = (args.grid + 1) * S + ws - 1
@@ -35,7 +36,7 @@ def main():
     lib = L.load()
     P1 = (S // 2) ** 2
     res = {v: [] for v in args.variants.split(',')}
-    outs = {}
+    outs, shas = {}, {}
     for rnd in range(args.rounds + 1):
         for v in res:
             fused = v == 'l12'       # dm_corr_level12 (level 2 fused, level 1 on chip); else level 1
@@ -59,13 +60,16 @@ def main():
                 res[v].append(e0.elapsed_time(e1))
             else:
                 outs[v] = l1[:2].cpu().numpy()
+                if args.sha:
+                    import hashlib
+                    shas[v] = hashlib.sha256(l1.cpu().numpy().tobytes()).hexdigest()[:16]
             del l1, pyr, batch
     ref = next(iter(outs.values()))
     for v, ts in res.items():
         same = outs[v].shape == ref.shape and np.array_equal(outs[v], ref, equal_nan=True)
-        print('%-8s median %8.3f ms  min %8.3f ms  (%s)  bit-identical to %s: %s'
-              % (v, np.median(ts), np.min(ts), ' '.join('%.2f' % t for t in ts),
-                 next(iter(outs)), same))
+        print('%-8s S=%d median %8.3f ms  min %8.3f ms  (%s)  bit-identical to %s: %s%s'
+              % (v, S, np.median(ts), np.min(ts), ' '.join('%.2f' % t for t in ts),
+                 next(iter(outs)), same, ('  sha256 ' + shas[v]) if v in shas else ''))
 
 
 if __name__ == '__main__':

@@ -18,26 +18,75 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EM_AMDGPU = 224
 
-# the kernel instance each profiled shape launches (mangled-name substrings, unique in the
-# library): (kind, tile, bytes per voxel or None) -> symbol
-LEVEL = {64: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',      # C2: 4 one-wave blocks per workgroup
-         128: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE',     # C3: GW = 4, 2 two-wave blocks
-         256: 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}     # C5: GW = 4, 4 waves
-# k_volume_ls<G, NW, NT, OT, TR, MW>: (tile, bytes per voxel, min/max known) -> instance
-# (dm_kernels.hip launch_volume_ls: DM_VL_H_* / DM_VL_F_* at w0 = 128, TR 0 elsewhere)
-VOLUME = {(128, 4, False): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E', (128, 4, True): 'k_volume_lsILi8ELi8ELb1EfLi4ELi4E',
-          (128, 2, False): 'k_volume_lsILi8ELi8ELb1EDF16_Li0ELi1E',
-          (128, 2, True): 'k_volume_lsILi8ELi4ELb1EDF16_Li2ELi1E',
-          (256, 4, False): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E', (256, 4, True): 'k_volume_lsILi16ELi8ELb1EfLi0ELi1E',
-          (256, 2, False): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E',
-          (256, 2, True): 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E'}
+# The kernel instance each profiled shape launches depends on the library's compile-time
+# switches (dm_kernels.hip: DM_S1, DM_C*_NB, DM_VL_*), which the library reports through
+# dm_build_config(); the symbols below are derived from it, so an A/B build made with -D
+# overrides (tools/abl_build.sh) is looked up under its own instances.  A library without
+# dm_build_config (before round 5) uses the round-4 instances (LEGACY).
+LEVEL = (64, 128, 256)       # profiled level-kernel tiles: C2, C3, C5
+VOLUME = ((128, 4, False), (128, 4, True), (128, 2, False), (128, 2, True),
+          (256, 4, False), (256, 4, True), (256, 2, False), (256, 2, True))
+DEFAULTS = {'S1': 1, 'C2_NB': 4, 'C3_NB': 2, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
+            'VL_H2_TR': 0, 'VL_H2_NW': 8, 'VL_F2_TR': 0, 'VL_F2_MW': 1, 'VL_HS_NW': 8, 'VL_F_NW': 8,
+            'VL_F_TR': 4, 'VL_F_MW': 4, 'VL_F_NT': 1}
+LEGACY = {('level', 64): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',
+          ('level', 128): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE',
+          ('level', 256): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}
+_CONFIG = {}
 
 
-def symbol(kind, tile, esz=None, mm=False):
+def _lib_path(lib=None):
+    return lib or os.environ.get('DM_LIB_PATH') or os.path.join(
+        REPO, 'deepmatching_stereo_matching_amd', 'libdmstereo.so')
+
+
+def build_config(lib=None):
+    """The library's compile-time switches as a dict (dm_build_config()); None if the library
+    cannot be loaded, {} if it predates dm_build_config."""
+    path = _lib_path(lib)
+    if path not in _CONFIG:
+        try:
+            import ctypes
+            h = ctypes.CDLL(path)
+        except OSError:
+            return None
+        try:
+            fn = h.dm_build_config
+        except AttributeError:
+            _CONFIG[path] = {}
+        else:
+            fn.restype = ctypes.c_char_p
+            _CONFIG[path] = {k: int(v) for k, v in (kv.split('=') for kv in fn().decode().split())}
+    return _CONFIG[path]
+
+
+def symbol(kind, tile, esz=None, mm=False, lib=None):
     """The symbol substring of the level kernel ('level') or a volume kernel ('volume', esz
-    bytes per voxel, min/max known or not) that a tile of side `tile` launches; None if not
-    profiled."""
-    return LEVEL.get(tile) if kind == 'level' else VOLUME.get((tile, esz, bool(mm)))
+    bytes per voxel, min/max known or not) that a tile of side `tile` launches in `lib` (the
+    loaded one by default); None if not profiled."""
+    cfg = build_config(lib)
+    if cfg == {} and kind == 'level':
+        return LEGACY.get((kind, tile))
+    c = dict(DEFAULTS, **(cfg or {}))
+    if kind == 'level':
+        if tile not in LEVEL:
+            return None
+        nb = c['C2_NB'] if tile == 64 else c['C3_NB'] if tile == 128 else c['C5_NB']
+        nw = nb * (1 if tile == 64 else 2 if tile == 128 else 4)
+        return 'k_level1_mfqILi1ELi4ELi%dELi4ELb1ELb1ELi%dELb1ELb%dEE' % (nw, nb, c['S1'])
+    if (tile, esz, bool(mm)) not in VOLUME:
+        return None
+    if tile == 128 and esz == 4:
+        return 'k_volume_lsILi8ELi%dELb%dEfLi%dELi%dE' % (c['VL_F_NW'], c['VL_F_NT'], c['VL_F_TR'], c['VL_F_MW'])
+    if tile == 128:
+        if mm:
+            return 'k_volume_lsILi8ELi%dELb%dEDF16_Li%dELi1E' % (c['VL_H_NW'], c['VL_H_NT'], c['VL_H_TR'])
+        return 'k_volume_lsILi8ELi%dELb1EDF16_Li0ELi1E' % c['VL_HS_NW']
+    if esz == 4:
+        return 'k_volume_lsILi16ELi8ELb1EfLi%dELi%dE' % (c['VL_F2_TR'], c['VL_F2_MW'])
+    if mm:
+        return 'k_volume_lsILi16ELi%dELb1EDF16_Li%dELi1E' % (c['VL_H2_NW'], c['VL_H2_TR'])
+    return 'k_volume_lsILi16ELi8ELb1EDF16_Li0ELi1E'
 
 
 def _elfs(data):
@@ -79,8 +128,7 @@ def kernel_hash(symbol_substring, lib=None):
     """sha256 (hex, 16 chars) of the machine code + kernel descriptor (less its code offset) of
     the ONE kernel whose mangled name contains `symbol_substring`; None if the library or the
     kernel is absent."""
-    lib = lib or os.environ.get('DM_LIB_PATH') or os.path.join(
-        REPO, 'deepmatching_stereo_matching_amd', 'libdmstereo.so')
+    lib = _lib_path(lib)
     try:
         data = open(lib, 'rb').read()
     except OSError:

@@ -5,7 +5,10 @@ matches; unmatched blocks take the weight of the nearest matched block before th
 result is checked the usual way: its instruction count against the PMC SQ_INSTS_VALU of a
 run of the new build.
 
-    python tools/remap_weights.py old.s OLD_KERNEL old_weights.json new.s NEW_KERNEL > new_weights.json
+    python tools/remap_weights.py old.s OLD_KERNEL old_weights.json new.s NEW_KERNEL [LABEL=N ...] > new.json
+
+LABEL=N arguments set a block's weight by hand (a block the alignment cannot match: new code,
+or a loop whose trip count changed).
 """
 import difflib
 import json
@@ -18,7 +21,7 @@ def sig(b):
     return tuple(sorted(b['ops'].items())) + (b['lds'], b['vmem'])
 
 
-def main(old_s, old_k, old_w, new_s, new_k):
+def main(old_s, old_k, old_w, new_s, new_k, *sets):
     ob = isa_cost.blocks(isa_cost.kernel_lines(old_s, old_k))
     nb = isa_cost.blocks(isa_cost.kernel_lines(new_s, new_k))
     w = json.load(open(old_w))
@@ -41,6 +44,10 @@ def main(old_s, old_k, old_w, new_s, new_k):
             v = last
         out[k] = v
         last = v
+    for kv in sets:
+        k, v = kv.split('=')
+        assert k in out, 'no block ' + k
+        out[k] = float(v) if '.' in v else int(v)
     if '_build' in w:
         out['_build'] = w['_build']
     json.dump(out, sys.stdout, indent=1)
@@ -48,4 +55,4 @@ def main(old_s, old_k, old_w, new_s, new_k):
 
 
 if __name__ == '__main__':
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:])
