@@ -63,6 +63,9 @@ SPEC_CLOCK_GHZ = 2.4           # MI355X_MICROARCH.md: max clock (the issue roofl
 # DM_BENCH_BACKEND=gloo and DM_BENCH_ONE_DEVICE=1 put every rank on cuda:0 over gloo.  The
 # driver's runs leave both unset: one rank per GPU over RCCL ("nccl").
 BACKEND = os.environ.get('DM_BENCH_BACKEND', 'nccl')
+# the c5 split solves each rank's band of tiles in this many chunks, each chunk's gather to rank 0
+# overlapping the next chunk's compute (shard.ChunkGather)
+C5_CHUNKS = int(os.environ.get('DM_C5_CHUNKS', '4'))
 ONE_DEVICE = os.environ.get('DM_BENCH_ONE_DEVICE', '0') == '1'
 VOLUME_BUDGET = 72e9           # bytes of level-0 volume materialised for its roofline: the whole
                                # C3 batch in float32 (68.7 GB), 8 S=256 tiles in fp16 (whole
@@ -108,6 +111,9 @@ def parse():
     ap.add_argument('--no-c5-split', action='store_true',
                     help='c3: skip the c5_split sub-line (one 4096^2 pair, tiles split over the ranks)')
     ap.add_argument('--c5-steps', type=int, default=3, help='timed steps of the c5_split sub-line')
+    ap.add_argument('--c5-no-group', action='store_true',
+                    help='N = 1: run the c5_split sub-line without the one-rank process group (no '
+                         'gather, no split_breakdown)')
     return ap.parse_args()
 
 
@@ -115,60 +121,95 @@ class PairSolver:
     """One ImageCutSolver-equivalent pass over a resident pair, with event timing of the
     dominant kernel (dm_corr_level12)."""
 
-    def __init__(self, img1, img2, tile, grid, split=False, levels=None):
-        """split: the pair's tiles are sharded over the ranks (rank r solves tiles r::N) and
-        the per-tile results are gathered to rank 0 (RCCL over xGMI), which stitches the map;
-        otherwise this rank solves every tile of its own pair.  levels: k-level pyramid
-        (None: the full pyramid)."""
+    def __init__(self, img1, img2, tile, grid, split=False, levels=None, chunks=None):
+        """split: the pair's tiles are sharded over the ranks of the process group (rank r
+        solves one contiguous band of tiles, shard.rank_band) and the per-tile results are
+        gathered to rank 0 (RCCL over xGMI), which stitches the map; the band is solved in
+        `chunks` chunks, each chunk's gather issued as soon as it is computed so it overlaps
+        the next chunk (shard.ChunkGather).  Otherwise this rank solves every tile of its own
+        pair in one batch.  levels: k-level pyramid (None: the full pyramid)."""
         from deepmatching_stereo_matching_amd import shard
         self.dev = img1.device
         self.tile = tile
         self.levels = levels
         self.n, origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
         assert self.n == [grid, grid], self.n
+        self.split = bool(split)
+        self.nchunks = chunks
         self.rank, self.world = shard.world() if split else (0, 1)
         self.T = len(origins)
-        self.origins = origins[shard.rank_units(self.T, self.rank, self.world)]
-        self.batch = engine.TileBatch(img1, img2, self.origins, tile, tile, WS,
-                                      L.DM_TM_CCOEFF_NORMED, self.dev)
-        self.ev = []
+        if self.split:
+            g = self._gather()
+            self.chunk_idx = [g.chunk_units(c) for c in range(g.chunks)]
+            self.origins = origins[shard.rank_band(self.T, self.rank, self.world)]
+        else:
+            self.chunk_idx = [list(range(self.T))]
+            self.origins = origins
+        self.batches = [engine.TileBatch(img1, img2, origins[idx], tile, tile, WS, L.DM_TM_CCOEFF_NORMED, self.dev)
+                        if idx else None for idx in self.chunk_idx]
+        self.batch = next((b for b in self.batches if b is not None), None)
+        self.ev = []        # per timed solve: [(start, end) of each chunk's level kernel]
+
+    def _gather(self):
+        from deepmatching_stereo_matching_amd import shard
+        return shard.ChunkGather(self.T, self.rank, self.world, (3, self.tile, self.tile), torch.float64,
+                                 self.dev, dst=0, chunks=self.nchunks or C5_CHUNKS)
 
     def step(self, timed=False, stream=None, wait=None, level_stream=None, stats_stream=None):
         """One full solve of the pair on `stream` (default: the current stream).  Every
-        device buffer belongs to this step's DevicePyramid, so steps on different streams
+        device buffer belongs to this step's DevicePyramids, so steps on different streams
         share only the read-only images.  `wait`: event the level kernel waits for (the
         previous solve's level-kernel end when solves are pipelined over streams); this
-        solve's level-kernel end is left in self.last_end."""
+        solve's last level-kernel end is left in self.last_end."""
         if stream is not None:
             with torch.cuda.stream(stream):
                 return self.step(timed=timed, wait=wait, level_stream=level_stream,
                                  stats_stream=stats_stream)
-        from deepmatching_stereo_matching_amd import shard
-        match = self.compute(timed=timed, wait=wait, level_stream=level_stream,
-                             stats_stream=stats_stream)
-        if self.world > 1:   # rank 0 receives every tile's (3, S, S) result and stitches
-            match = shard.gather_units_to(match, self.T, self.rank, self.world, 0)
+        if self.split:   # rank 0 receives every tile's (3, S, S) result and stitches
+            g = self._gather()
+            self.compute(timed=timed, wait=wait, level_stream=level_stream, stats_stream=stats_stream, gather=g)
+            match = g.result()
             if match is None:
                 return None
+        else:
+            match = self.compute(timed=timed, wait=wait, level_stream=level_stream,
+                                 stats_stream=stats_stream)
         return engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                              ['elevation'])
 
-    def compute(self, timed=False, wait=None, level_stream=None, stats_stream=None):
-        """This rank's tiles: stats, dm_corr_level12 [timed], dm_aggregate levels 3.., matching
-        with sub-pixel -> float64 [T_rank][3][S][S] on the current stream."""
-        pyr = engine.DevicePyramid(self.batch, build=False, stats_stream=stats_stream)
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    def compute(self, timed=False, wait=None, level_stream=None, stats_stream=None, gather=None):
+        """This rank's tiles, chunk by chunk: stats, dm_corr_level12 [timed], dm_aggregate
+        levels 3.., matching with sub-pixel -> float64 [T_chunk][3][S][S] on the current
+        stream; with `gather` each chunk's result is handed to it (put) as soon as it is
+        issued, else the one chunk's result is returned."""
+        evs, out = [], None
+        for c, b in enumerate(self.batches):
+            if b is None:   # a rank with fewer tiles than the others: an empty chunk
+                out = torch.empty((0, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
+            else:
+                pyr = engine.DevicePyramid(b, build=False, stats_stream=stats_stream)
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                evs.append(ev)
+                self.last_end = ev[1]
+                diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
+                pyr.build(events=ev, wait=wait if c == 0 else None,
+                          nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
+                if diag:
+                    out = torch.zeros((b.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
+                else:
+                    out = pyr.match(sub_pix=True, nlev=self.levels)
+            if gather is not None:
+                gather.put(c, out)
         if timed:
-            self.ev.append(ev)
-        self.last_end = ev[1]
-        diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
-        pyr.build(events=ev, wait=wait, nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
-        if diag:
-            return torch.zeros((self.batch.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
-        return pyr.match(sub_pix=True, nlev=self.levels)
+            self.ev.append(evs)
+        return out
 
     def level1_ms(self):
-        return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else None
+        """Mean over the timed solves of the level-kernel time per solve (summed over its
+        chunks)."""
+        if not self.ev:
+            return None
+        return float(np.mean([sum(a.elapsed_time(b) for a, b in evs) for evs in self.ev]))
 
 
 def volume_roofline(solver, reps=3, f16=False):
@@ -419,29 +460,31 @@ def volume_equivalent(solver, tile, l1_ms):
 
 
 def split_breakdown(solver, rank, world, dev):
-    """c5 split: one more (untimed) solve, instrumented per rank -- compute (this rank's tiles:
-    pyramid + matching), gather to rank 0, stitch (rank 0) -- in ms, for every rank."""
+    """c5 split: one more (untimed) solve, instrumented per rank -- compute (this rank's band of
+    tiles, chunk by chunk: pyramid + matching, each chunk's gather to rank 0 issued behind it),
+    the wait for the gathers still in flight when the compute ends, stitch (rank 0) -- in ms,
+    for every rank."""
     import torch.distributed as tdist
-    from deepmatching_stereo_matching_amd import shard
     torch.cuda.synchronize()
     tdist.barrier()
     t0 = time.perf_counter()
-    match = solver.compute()
+    g = solver._gather()
+    solver.compute(gather=g)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    full = shard.gather_units_to(match, solver.T, rank, world, 0)
+    full = g.result()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     if full is not None:
         engine.stitch(full, solver.n, solver.tile, solver.tile, [solver.tile, solver.tile], ['elevation'])
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    mine = torch.tensor([t1 - t0, t2 - t1, t3 - t2, float(len(solver.origins))], dtype=torch.float64,
-                        device=dev if BACKEND == 'nccl' else 'cpu')
+    mine = torch.tensor([t1 - t0, t2 - t1, t3 - t2, float(len(solver.origins)), float(g.chunks)],
+                        dtype=torch.float64, device=dev if tdist.get_backend() == 'nccl' else 'cpu')
     parts = [torch.empty_like(mine) for _ in range(world)]
     tdist.all_gather(parts, mine)
-    return [{'rank': r, 'tiles': int(p[3]), 'compute_ms': round(float(p[0]) * 1e3, 3),
-             'gather_ms': round(float(p[1]) * 1e3, 3), 'stitch_ms': round(float(p[2]) * 1e3, 3)}
+    return [{'rank': r, 'tiles': int(p[3]), 'chunks': int(p[4]), 'compute_ms': round(float(p[0]) * 1e3, 3),
+             'gather_wait_ms': round(float(p[1]) * 1e3, 3), 'stitch_ms': round(float(p[2]) * 1e3, 3)}
             for r, p in enumerate(parts)]
 
 
@@ -611,21 +654,27 @@ def c5_split(args, rank, world, dev, dist):
     del a, b
     voxels = grid * grid * float(tile) ** 4
     steps, warmup = args.c5_steps, 1
-    solver = PairSolver(img1, img2, tile, grid, split=world > 1)
+    # with a process group (N > 1, or the one-rank RCCL group main() starts at N = 1) the tiles
+    # go through the split path: bands, chunked gathers to rank 0
+    from deepmatching_stereo_matching_amd import shard
+    split = world > 1 or shard.world()[1] == 1 and shard._group()
+    solver = PairSolver(img1, img2, tile, grid, split=split)
     pipe = Pipeline([solver], dev, dist, nstreams=max(1, args.streams), chain_levels=args.chain_levels)
     held = [] if not args.no_step_check else None
     el = pipe.run(steps, warmup, hold=held)
     ms = el / steps * 1e3
     out = {'workload': 'C5: one %dx%d pair per step, %dx%d tiles of S=%d, ws=%d, full pyramid + '
-                       'sub-pixel + cal_map + stitch; tiles split %d-way, gathered to rank 0'
-                       % (grid * tile, grid * tile, grid, grid, tile, WS, world),
+                       'sub-pixel + cal_map + stitch; tiles split %d-way in contiguous bands, each '
+                       'band in %d chunks gathered to rank 0 behind the compute%s'
+                       % (grid * tile, grid * tile, grid, grid, tile, WS, world,
+                          len(solver.chunk_idx), ' (RCCL process group of one rank)' if world == 1 and split else ''),
            'n_gpus': world, 'steps': steps, 'warmup': warmup, 'ms_per_pair': round(ms, 3),
            'value': round(voxels / (ms * 1e-3) / 1e9, 3), 'unit': 'Gvox/s',
            'level_kernel_ms': round(solver.level1_ms(), 3) if solver.ev else None}
     if held is not None:
         out['step_outputs'] = check_step_outputs(held, [solver], dist, steps)
         del held
-    if world > 1:
+    if split:
         out['split_breakdown'] = split_breakdown(solver, rank, world, dev)
     del pipe, solver
     torch.cuda.empty_cache()
@@ -792,7 +841,21 @@ def main():
     if args.config == 'c3' and not args.no_c5_split and args.tile is None and args.grid is None:
         del pipe
         torch.cuda.empty_cache()
+        own_group = False
+        if not dist and not args.c5_no_group:
+            # N = 1: a one-rank process group (RCCL with the default backend), so the c5 split's
+            # band / chunked-gather path and its split_breakdown run at N = 1 too
+            import socket
+            import torch.distributed as tdist
+            with socket.socket() as sk:
+                sk.bind(('127.0.0.1', 0))
+                port = sk.getsockname()[1]
+            kw = {'device_id': dev} if BACKEND == 'nccl' else {}
+            tdist.init_process_group(BACKEND, init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1, **kw)
+            own_group = True
         c5 = c5_split(args, rank, world, dev, dist)
+        if own_group:
+            tdist.destroy_process_group()
         if rank == 0:
             rec['c5_split'] = c5
     if rank == 0:

@@ -178,32 +178,57 @@ __global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
     }
 }
 
-// A operand of the strip MFMA: lane L, row i = L & 31 = patch i & 15 of the 2 x 2 cell block
-// (cell (i & 15) >> 2, child i & 3, as build_a's row c) at strip offset i >> 4
-// (WSC: ws known at compile time -- the byte loads unrolled and issued together; 0 = g.ws)
-template <int WSC>
-__device__ __forceinline__ dm_v4i build_a_strip(const Geo &g, int t, int I0, int J0, int lane)
+// XCD-aware workgroup order (DM_XCD_MAP): workgroups are dealt round robin over the 8 XCDs
+// (MI355X_MICROARCH.md, workgroup dispatch), so consecutive workgroups -- the cell blocks of one
+// tile, which read the same window operands -- land on 8 different L2s.  With the grid a
+// multiple of 8, workgroup b is given logical index (b % 8) * (grid / 8) + b / 8: each XCD then
+// walks one contiguous range of blocks, i.e. whole tiles in order, and the tile's window
+// operands stay in that XCD's L2 (placement only: any order is correct).
+#ifndef DM_XCD_MAP
+#define DM_XCD_MAP 1
+#endif
+__device__ __forceinline__ int wg_logical()
 {
-    const int ws = WSC ? WSC : g.ws, NS = (ws + 1) * ws;
-    const int i = lane & 31, h = lane >> 5, pi = i & 15, o = i >> 4;
-    const int cl = pi >> 2, ch = pi & 3;
-    const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
-    // byte loads at 32-bit offsets from the tile's origin (one uniform buffer resource), every
-    // byte from a clamped in-patch address and then kept or zeroed: no 64-bit address per
-    // byte, no branch, the 16 loads in flight together
+    const int b = blockIdx.x, n = gridDim.x;
+    if (!DM_XCD_MAP || (n & 7)) return b;
+    return (b & 7) * (n >> 3) + (b >> 3);
+}
+
+// The workgroup's patch taps in LDS (S1 instances): ptab[sb][patch][0..7] = the 16 patches' taps
+// 0 .. 31 as int8 (zero from n on), [8..15] the same shifted by ws bytes (ws zero bytes, then
+// the taps): exactly the K bytes of the strip MFMA's A rows (offset 0 and 1), and the first copy
+// holds build_a's spread fragments (taps 8 grp .. 8 grp + 7).  One pass of the workgroup's
+// threads (a dword each: 4 byte loads through the tile's buffer resource) replaces every lane's
+// own 16 + 8 byte loads and address arithmetic.
+template <int NB, int NT, int WSC>
+__device__ __forceinline__ void fill_ptab(unsigned (&ptab)[NB][16][16], const Geo &g, int tid, int bpt, int nbj)
+{
+    const int ws = WSC ? WSC : g.ws, n = ws * ws;
+    const int blk0 = wg_logical() * NB;
+    const int t = blk0 / bpt; // bpt % NB == 0: every block of the workgroup is in tile t
     const __amdgpu_buffer_rsrc_t rI = tile_rsrc(g.img1, g.pitch1, g, t);
-    const unsigned pb = (unsigned)(p0 * g.pitch1 + p1);
-    int w[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int k = 16 * h + j;
-        const int row = k / ws - o, col = k % ws;
-        const bool in = k < NS && row >= 0 && row < ws;
-        const int rc = row < 0 ? 0 : (row >= ws ? ws - 1 : row);
-        const int v = (int)__builtin_amdgcn_raw_buffer_load_b8(rI, pb + (unsigned)(rc * g.pitch1 + (k < NS ? col : 0)), 0, 0) - 128;
-        w[j >> 2] |= ((in ? v : 0) & 0xFF) << (8 * (j & 3));
+    for (int e0 = 0; e0 < NB * 256; e0 += NT) {
+        const int e = e0 + tid;
+        if (NB * 256 % NT != 0 && e >= NB * 256) break;
+        const int sb = e >> 8, pi = (e >> 4) & 15, d = e & 15;
+        const int blk = blk0 + sb;
+        const int I0 = 2 * ((blk % bpt) / nbj), J0 = 2 * ((blk % bpt) % nbj);
+        const int cl = pi >> 2, ch = pi & 3;
+        const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+        const unsigned pb = (unsigned)(p0 * g.pitch1 + p1);
+        const int o = d >> 3, k0 = 4 * (d & 7);
+        unsigned w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int tau = k0 + b - ws * o;
+            const bool in = tau >= 0 && tau < n;
+            const int tc = tau < 0 ? 0 : (tau >= n ? n - 1 : tau);
+            const int v = (int)__builtin_amdgcn_raw_buffer_load_b8(rI, pb + (unsigned)((tc / ws) * g.pitch1 + tc % ws), 0, 0) - 128;
+            w |= (unsigned)((in ? v : 0) & 0xFF) << (8 * b);
+        }
+        ptab[sb][pi][d] = w;
     }
-    return dm_v4i{w[0], w[1], w[2], w[3]};
 }
 
 // min of mn[k] / max of mx[k] over the 32 lanes of each half-wave by DPP: row rotations 8, 4, 2,
@@ -473,7 +498,8 @@ struct XchOwn<true, T, OFF> {
 // waves sb * NWc .. sb * NWc + NWc - 1 split block sb's columns; the blocks share the pow
 // tables, which is what a workgroup of more than one wave buys there.
 // S1: sweep 1 on the row-pair strips (Bs, Ss: k_prep_strips) with the 32 x 32 x 32 i8 MFMA --
-// half the matrix-core issue cycles of the 16 x 16 tiles per voxel, and the window stats
+// half the matrix-core issue cycles of the 16 x 16 tiles per voxel (A rows from the LDS tap table,
+// fill_ptab), and the window stats
 // broadcast without copies; sweep 2 keeps the 16 x 16 layout its pooling needs.
 template <int KS, int GW, int NW, int MINW, bool L2F, bool YF, int NB = 1, bool CL = false, bool S1 = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
@@ -523,6 +549,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     pow_lds_fill(plds, tid, 64 * NW, HOLE);
     if (NWc > 1 && tid < 64 * NB)
         (&xch[tid >> 6][0][0][0][0][0])[((tid & 63) >> 4) * XS * 16 + (tid & 15)] = -INFINITY;
+    __shared__ __attribute__((aligned(16))) unsigned ptab[S1 ? NB : 1][16][16];
+    if constexpr (S1) {
+        const int nbj_ = (g.w0 / 2) / 2, bpt_ = ((g.h0 / 2) / 2) * nbj_;
+        if (g.ws == 5) fill_ptab<S1 ? NB : 1, 64 * NW, 5>(ptab, g, tid, bpt_, nbj_);
+        else fill_ptab<S1 ? NB : 1, 64 * NW, 0>(ptab, g, tid, bpt_, nbj_);
+    }
     __syncthreads();
 
     constexpr int G = GW * NWc;
@@ -534,7 +566,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     const int h0 = g.h0, w0 = g.w0, n = g.ws * g.ws, P = h0 * w0;
     const int w1 = w0 / 2, P1 = (h0 / 2) * w1;
     const int nbj = w1 / 2, bpt = ((h0 / 2) / 2) * nbj; // 2x2-cell blocks per tile
-    const int blk = blockIdx.x * NB + sb;
+    const int blk = wg_logical() * NB + sb;
     const int t = blk / bpt;                             // whole workgroup in range (grid exact)
     const int I0 = 2 * ((blk % bpt) / nbj), J0 = 2 * ((blk % bpt) % nbj);
     const size_t tb = (size_t)t * P;
@@ -547,8 +579,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     // the 16 x 16 tiles' patch operand and sums (S1: built after the strip sweep, which does
     // not read them -- they would hold registers through it)
     auto init_a16 = [&]() {
-        if (g.ws == 5) build_a<KS, 5>(A, g, t, I0, J0, c, grp);
-        else build_a<KS>(A, g, t, I0, J0, c, grp);
+        if constexpr (S1) { // the spread fragment: taps 8 grp .. 8 grp + 7 of patch row c (ptab)
+            const dm_v2i tp = *(const dm_v2i *)&ptab[sb][c][2 * grp];
+            A[0] = dm_v4i{tp.x, tp.y, 0, 0};
+        } else {
+            build_a<KS>(A, g, t, I0, J0, c, grp);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = (2 * Ic + (r >> 1)) * w0 + 2 * Jc + (r & 1);
@@ -612,7 +648,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
         // this wave's windows: strip tiles 2 wc, 2 wc + 1 (32 columns each) of every row pair;
         // lane (c32, hs) holds cells hs, 2 + hs of the block at window column c32, both rows
         const int c32 = lane & 31, hs = lane >> 5;
-        const dm_v4i A32 = g.ws == 5 ? build_a_strip<5>(g, t, I0, J0, lane) : build_a_strip<0>(g, t, I0, J0, lane);
+        const dm_v4i A32 = *(const dm_v4i *)&ptab[sb][lane & 15][8 * ((lane >> 4) & 1) + 4 * hs]; // row L & 31: offset (L >> 4) & 1
         float sTs[8]; // [cell slot cs][child]: cell 2 cs + hs
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -836,6 +872,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 
     // rows in pairs (q0 even, q0 + 1 odd) = level-1 row u = q0 / 2; one barrier per pair
     // publishes both rows' edge values and the previous pair's level-1 edge value
+    // (measured: two pairs per iteration with the parity at compile time models 2.7 % MORE
+    // issue cycles -- the compiler splits and spreads the first pair's MFMA block)
     for (int q0 = 0; q0 < h0; q0 += 2) {
         const int u = q0 >> 1, k = u & 1;
         load_row(fb, q0 + 1);

@@ -63,13 +63,33 @@ def rank_units(n, rank, size):
     return list(range(rank, n, size))
 
 
+def rank_band(n, rank, size):
+    """Units of this rank: one contiguous band [n r / N, n (r + 1) / N) (balanced to within one
+    unit).  For the tiles of one pair, a band is a run of whole tile columns (ImageCutSolver's
+    tile order), so a rank's image reads are one contiguous region instead of N-strided tiles."""
+    return list(range(n * rank // size, n * (rank + 1) // size))
+
+
+def _collective(size):
+    """Run the collective?  Only with a process group, and only when `size` is that group's
+    size: a caller passing another size while a group of N ranks is initialised would enter a
+    collective whose parts list does not match the group."""
+    if not _group():
+        if size != 1:
+            raise ValueError('no process group for a %d-rank gather' % size)
+        return False
+    if size != dist.get_world_size():
+        raise ValueError('gather over %d ranks inside a process group of %d' % (size, dist.get_world_size()))
+    return True
+
+
 def _gather_units(local, n, rank, size, shape, dtype):
     """All-gather per-rank unit results ([k_r][*shape]) back into unit order [n][*shape].
     With the nccl (RCCL) backend the gather runs device to device over xGMI; a gloo group
     (CPU tests, or ranks sharing one GPU) gathers host copies and the result goes back to
     ``local``'s device."""
     per = (n + size - 1) // size
-    group = _group()
+    group = _collective(size)
     host = group and local.is_cuda and dist.get_backend() == 'gloo'
     dev = local.device
     buf = torch.zeros((per,) + tuple(shape), dtype=dtype, device='cpu' if host else dev)
@@ -87,15 +107,16 @@ def _gather_units(local, n, rank, size, shape, dtype):
     return out.to(dev) if host else out
 
 
-def gather_units_to(local, n, rank, size, dst=0):
-    """Gather per-rank unit results ([k_r][*shape], units r::N) to rank ``dst`` only, in unit
-    order [n][*shape]; the other ranks get None.  Only the rank that stitches receives the
-    tiles: with nccl (RCCL over xGMI) each peer sends its k_r units device to device, one link
-    per peer, instead of every rank receiving every unit (all-gather).  gloo gathers host
-    copies; the result goes back to ``local``'s device."""
+def gather_units_to(local, n, rank, size, dst=0, units=rank_units):
+    """Gather per-rank unit results ([k_r][*shape], the units ``units(n, r, size)`` of rank r:
+    round robin by default, rank_band for bands) to rank ``dst`` only, in unit order
+    [n][*shape]; the other ranks get None.  Only the rank that stitches receives the tiles:
+    with nccl (RCCL over xGMI) each peer sends its k_r units device to device, one link per
+    peer, instead of every rank receiving every unit (all-gather).  gloo gathers host copies;
+    the result goes back to ``local``'s device."""
     shape, dtype = tuple(local.shape[1:]), local.dtype
-    per = (n + size - 1) // size
-    group = _group()
+    per = max(len(units(n, r, size)) for r in range(size))
+    group = _collective(size)
     host = group and local.is_cuda and dist.get_backend() == 'gloo'
     dev = local.device
     if len(local) == per and not host:
@@ -112,10 +133,73 @@ def gather_units_to(local, n, rank, size, dst=0):
         return None
     out = torch.empty((n,) + shape, dtype=dtype, device=buf.device)
     for r in range(size):
-        k = len(rank_units(n, r, size))
-        if k:
-            out[r::size] = parts[r][:k]
+        idx = units(n, r, size)
+        if idx:
+            out[idx] = parts[r][:len(idx)]
     return out.to(dev) if host else out
+
+
+class ChunkGather:
+    """The units of every rank gathered to rank ``dst`` chunk by chunk, each chunk's gather
+    issued (asynchronously) as soon as the rank has computed it, so it travels over xGMI while
+    the rank computes its next chunk; only the last chunk's transfer is left when the rank's
+    compute ends.  Rank r's units are ``units(n, r, size)`` (contiguous bands by default), cut
+    into ``chunks`` chunks of equal count (every rank issues the same number of collectives,
+    shorter ones padded).  put(c, local) for c = 0 .. chunks - 1 in order on every rank, then
+    result() -> [n][*shape] on dst, None elsewhere.  Without a process group (size 1) the
+    chunks are assembled locally."""
+
+    def __init__(self, n, rank, size, shape, dtype, device, dst=0, chunks=1, units=rank_band):
+        self.n, self.rank, self.size, self.dst = n, rank, size, dst
+        self.shape, self.dtype = tuple(shape), dtype
+        self.units = units
+        self.per = max(len(units(n, r, size)) for r in range(size))
+        self.chunks = max(1, min(int(chunks), self.per)) if self.per else 1
+        self.csz = (self.per + self.chunks - 1) // self.chunks if self.per else 0
+        self.group = _collective(size)
+        self.host = self.group and torch.device(device).type == 'cuda' and dist.get_backend() == 'gloo'
+        self.device = torch.device(device)
+        self.work, self.parts, self.bufs = [], [], []
+
+    def chunk_units(self, c, r=None):
+        """Unit indices of chunk c of rank r (default: this rank)."""
+        idx = self.units(self.n, self.rank if r is None else r, self.size)
+        return idx[c * self.csz:(c + 1) * self.csz]
+
+    def put(self, c, local):
+        k = len(self.chunk_units(c))
+        assert local.shape[0] == k, (local.shape, k)
+        if not self.group:
+            self.parts.append([local])
+            return
+        dev = 'cpu' if self.host else self.device
+        if k == self.csz and not self.host:
+            buf = local.contiguous()
+        else:
+            buf = torch.zeros((self.csz,) + self.shape, dtype=self.dtype, device=dev)
+            if k:
+                buf[:k] = local
+        parts = [torch.empty_like(buf) for _ in range(self.size)] if self.rank == self.dst else None
+        self.bufs.append(buf)               # kept alive until the collective has completed
+        self.parts.append(parts)
+        self.work.append(dist.gather(buf, parts, dst=self.dst, async_op=True))
+
+    def result(self):
+        for w in self.work:
+            w.wait()
+        self.work, self.bufs = [], []
+        if self.rank != self.dst:
+            self.parts = []
+            return None
+        out = torch.empty((self.n,) + self.shape, dtype=self.dtype,
+                          device='cpu' if self.host else self.device)
+        for c, parts in enumerate(self.parts):
+            for r in range(self.size if self.group else 1):
+                idx = self.chunk_units(c, r if self.group else self.rank)
+                if idx:
+                    out[idx] = parts[r][:len(idx)]
+        self.parts = []
+        return out.to(self.device) if self.host else out
 
 
 def solve_tiles_sharded(img1, img2, origins, h0, w0, ws, method, sub_pix=True, filtering=False,

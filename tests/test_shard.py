@@ -175,3 +175,71 @@ def test_tile_sharding_is_opt_in(monkeypatch):
             assert shard._TILE_SHARDING is False
         assert shard._TILE_SHARDING is True
     assert shard._TILE_SHARDING is None
+
+
+def test_rank_band_partition():
+    """Contiguous bands: every unit once, in order, balanced to within one unit."""
+    for n in (0, 1, 7, 64, 256):
+        for size in (1, 2, 3, 8):
+            bands = [shard.rank_band(n, r, size) for r in range(size)]
+            assert sum(bands, []) == list(range(n))
+            assert all(b == list(range(b[0], b[-1] + 1)) for b in bands if b)
+            counts = [len(b) for b in bands]
+            assert max(counts) - min(counts) <= 1
+
+
+def _chunk_worker(rank, size, port, n, chunks, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=size)
+    try:
+        g = shard.ChunkGather(n, rank, size, (2, 3), torch.float64, 'cpu', dst=0, chunks=chunks)
+        for c in range(g.chunks):
+            idx = g.chunk_units(c)
+            local = torch.tensor([[[float(i)] * 3] * 2 for i in idx], dtype=torch.float64).reshape(len(idx), 2, 3)
+            g.put(c, local)
+        out = g.result()
+        band = shard.rank_band(n, rank, size)
+        local = torch.tensor([[[float(i)] * 3] * 2 for i in band], dtype=torch.float64).reshape(len(band), 2, 3)
+        once = shard.gather_units_to(local, n, rank, size, 0, units=shard.rank_band)
+        bad = None
+        try:
+            shard.gather_units_to(local, n, rank, 1, 0)      # a size that is not the group's
+        except ValueError as e:
+            bad = str(e)
+        q.put((rank, None if out is None else out.numpy(), None if once is None else once.numpy(), g.chunks, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('size,n,chunks', [(2, 256, 4), (3, 256, 4), (3, 10, 4), (2, 3, 2)])
+def test_chunk_gather_bands(size, n, chunks):
+    """ChunkGather (bands cut into chunks, one asynchronous gather per chunk) and the one-shot
+    band gather deliver every unit to rank 0 in unit order; a gather over a size other than
+    the process group's raises instead of entering a mismatched collective."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, size, port, n, chunks, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(size))
+    for p in procs:
+        p.join(60)
+    want = np.repeat(np.arange(n, dtype=np.float64), 6).reshape(n, 2, 3)
+    for rank, out, once, nch, bad in res:
+        assert bad is not None and 'group' in bad
+        if rank == 0:
+            assert np.array_equal(out, want) and np.array_equal(once, want)
+        else:
+            assert out is None and once is None
+    assert len({r[3] for r in res}) == 1
+
+
+def test_chunk_gather_without_group():
+    g = shard.ChunkGather(5, 0, 1, (1,), torch.float64, 'cpu', chunks=2)
+    for c in range(g.chunks):
+        idx = g.chunk_units(c)
+        g.put(c, torch.tensor(idx, dtype=torch.float64).reshape(-1, 1))
+    assert torch.equal(g.result(), torch.arange(5, dtype=torch.float64).reshape(5, 1))
+    with pytest.raises(ValueError):
+        shard.gather_units_to(torch.zeros((2, 1)), 4, 0, 2)

@@ -13,13 +13,14 @@
 #   f4m, f4mp, f2mp, f4p, f0p   the w0 = 128 float32 volume: runs of 4 / 2 / none, m = compiled
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
 #   s0      sweep 1 on the 16 x 16 tiles instead of the row-pair strips (DM_S1=0; results exact)
+#   x0      the level kernel's workgroups in dispatch order, not XCD-grouped (DM_XCD_MAP=0; exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
 #   c5h2w4, c5f4m   the w0 = 256 volumes: binary16 min/max known with 2 x 512-B runs in
 #           4-wave workgroups; float32 with 1-KB runs at 4 waves/SIMD (DM_VL_H2_*, DM_VL_F2_*)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
 #           instead of 4 (DM_C2_NB; results exact)
-#   c3nb1   the S = 128 level kernel with 1 two-wave cell block per workgroup instead of 2
+#   c3nb1, c3nb4   the S = 128 level kernel with 1 / 4 two-wave cell blocks per workgroup instead of 2
 #   c5nb2   the S = 256 level kernel with 2 four-wave cell blocks per workgroup instead of 1
 #           (DM_C3_NB / DM_C5_NB; results exact)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
@@ -90,9 +91,11 @@ PY
     c5f4m) EXTRA="-DDM_VL_F2_TR=4 -DDM_VL_F2_MW=4" ;;
     c2nb2) EXTRA="-DDM_C2_NB=2" ;;
     c3nb1) EXTRA="-DDM_C3_NB=1" ;;
+    c3nb4) EXTRA="-DDM_C3_NB=4" ;;
     c5nb2) EXTRA="-DDM_C5_NB=2" ;;
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
     s0) EXTRA="-DDM_S1=0" ;;
+    x0) EXTRA="-DDM_XCD_MAP=0" ;;
     head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
           (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
              case $f in include/*) git show HEAD:$f > $r/$f ;; *) git show HEAD:$f > $d/csrc/$(basename $f) ;; esac; done) ;;
