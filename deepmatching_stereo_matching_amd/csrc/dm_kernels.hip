@@ -93,14 +93,23 @@ __device__ __forceinline__ void pow_lds_fill(PowLds &t, int tid, int nthreads, b
     }
 }
 
+// fma(a, b, c) with the constant c read from an SGPR pair by the VOP3 form: left to itself the
+// compiler keeps the polynomial's constants in VGPR pairs (for v_fmac_f64's tied addend) hoisted
+// out of the level kernels' loops -- 8 VGPRs held for a pow that runs once per row pair
+__device__ __forceinline__ double fma_sc(double a, double b, double c)
+{
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 // dm_pow14_fast's arithmetic from r = fma(M, c_i, -1), table index i and 2^(yE) row G = {G, g}
 __device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const PowLds &t)
 {
-    double q = DM_POWF_B5;
-    q = fma(q, r, DM_POWF_B4);
-    q = fma(q, r, DM_POWF_B3);
-    q = fma(q, r, DM_POWF_B2);
-    q = fma(q, r, DM_POWF_B1);
+    double q = fma_sc(r, DM_POWF_B5, DM_POWF_B4);
+    q = fma_sc(q, r, DM_POWF_B3);
+    q = fma_sc(q, r, DM_POWF_B2);
+    q = fma_sc(q, r, DM_POWF_B1);
     q = fma(q, r, G.y);
     const dm_d2 Pr = t.fp[i];
     const double s = fma(Pr.x, q, Pr.y) * G.x;
@@ -349,6 +358,7 @@ __device__ double l1_value(const Geo &g, const Stats &s, int t, int I, int J, in
 }
 
 #include "dm_mfma.h"
+#include "dm_strip.h"
 
 // ------------------------------------------------------------------------------------
 // K2 (generic): one workgroup per level-1 cell (= 2x2 block of patches p).  For each
@@ -1265,6 +1275,22 @@ static bool strip_shape(const dm_tiles *b)   // sizes the workspace: no environm
     return G % 4 == 0 && (G / 4 == 1 || G / 4 == 2 || G / 4 == 4);
 }
 
+// both sweeps on the strips (k_level12_strip, dm_strip.h) for the strip shapes whose bit is set
+// in DM_S2 (1: w0 = 64, C2; 2: w0 = 128, C3; 4: w0 = 256, C5); dm_corr_stats then skips the
+// 16 x 16 window operands (k_prep_windows16), which nothing else reads there.  Same box, bit-
+// identical (profiles/r05_strip_ab.txt): C5 27.06 / 27.04 ms against 27.44 / 27.30, C2 0.498
+// against 0.504 ms (mean of 4), C3 7.30 / 7.32 against 7.19 / 7.18 -- there k_level1_mfq stays
+// (the strip kernel issues 3.6 % more VALU instructions and 29 % more LDS ones per launch: its
+// lane holds two cells' normalisation constants and carries two windows' odd rows; fewer MFMA
+// cycles do not make up for it at 4 waves per SIMD, and at 3 the lost occupancy costs more)
+#ifndef DM_S2
+#define DM_S2 5
+#endif
+static bool strip2_shape(const dm_tiles *b)
+{
+    return strip_shape(b) && ((DM_S2 >> (b->w0 == 64 ? 0 : b->w0 == 128 ? 1 : 2)) & 1);
+}
+
 static size_t strip_bytes(const dm_tiles *b)
 {
     const size_t rows = (size_t)b->T * (b->h0 / 2);
@@ -1434,6 +1460,9 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 #ifndef DM_C5_NB
 #define DM_C5_NB 1   // four-wave cell blocks per workgroup of the S = 256 level kernel
 #endif
+#ifndef DM_C3_MW
+#define DM_C3_MW 4   // waves per SIMD the S = 128 strip kernel is compiled for
+#endif
 #ifndef DM_C3_NB
 #define DM_C3_NB 2   // two-wave cell blocks per workgroup of the S = 128 level kernel
 #endif
@@ -1455,7 +1484,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C5_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        if (Bs) k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        if (Bs && (DM_S2 & 4)) k_level12_strip<4, NBc, L2F, CL, 4><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
+        else if (Bs) k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
@@ -1468,7 +1498,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C2_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        if (Bs) k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        if (Bs && (DM_S2 & 1)) k_level12_strip<1, NBc, L2F, CL, 4><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
+        else if (Bs) k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
@@ -1479,7 +1510,8 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         constexpr int NBc = DM_C3_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
-        if (Bs) k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        if (Bs && (DM_S2 & 2)) k_level12_strip<2, NBc, L2F, CL, DM_C3_MW><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
+        else if (Bs) k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
@@ -1655,7 +1687,7 @@ int dm_abi_version(void) { return 109; }
 #define DM_STR(x) DM_STR2(x)
 const char *dm_build_config(void)
 {
-    return "S1=" DM_STR(DM_S1) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C5_NB=" DM_STR(DM_C5_NB)
+    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C5_NB=" DM_STR(DM_C5_NB)
            " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
            " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
            " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_F_NW=" DM_STR(DM_VL_F_NW)
@@ -1694,9 +1726,11 @@ int dm_corr_stats(const dm_tiles *b, void *d_stats, void *stream)
         const int G = b->w0 / 16, KS = (b->ws * b->ws + 63) / 64;
         const size_t n = (size_t)b->T * b->h0 * G * 16;
         const int GW = G / mfq_nw(b);
-        if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
-        else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
-        HIP_TRY(hipGetLastError());
+        if (!strip2_shape(b)) {
+            if (b->ws == 5) k_prep_windows16<5><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
+            else k_prep_windows16<0><<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(make_geo(b), G, GW, KS, Bw, QS);
+            HIP_TRY(hipGetLastError());
+        }
         if (strip_shape(b)) {
             dm_v4i *Bs, *Ss;
             strip_views(b, d_stats, &Bs, &Ss);

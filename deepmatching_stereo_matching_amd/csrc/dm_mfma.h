@@ -113,8 +113,11 @@ __global__ void k_prep_windows16(Geo g, int G, int GW, int KS, dm_v4i *Bw, int2 
 // the gfx950 32x32x32 i8 MFMA: lane L holds row / column L & 31, bytes 16 (L >> 5) .. +15 of
 // K (the same byte order for A and B, which is all a dot product needs); result register r
 // of lane L is C[8 (r >> 2) + 4 (L >> 5) + (r & 3)][L & 31].
-//   Bs[t][rp][q1 / 32][lane]  16 B: strip taps 16 (lane >> 5) .. +15 of window column
-//                             q1 = 32 (q1 / 32) + (lane & 31), rows q0 = 2 rp .. q0 + ws
+//   Bs[t][rp][tile][lane]     16 B: strip taps 16 (lane >> 5) .. +15 of window column
+//                             q1 = 64 (tile / 2) + 2 (lane & 31) + (tile & 1), rows q0 = 2 rp ..
+//                             q0 + ws: the two tiles of a 64-window group interleave their
+//                             columns, so lane c32 holds windows 2 c32 and 2 c32 + 1 of the
+//                             group (the column pooling of k_level12_strip stays in the lane)
 //   Ss[t][rp][q1]             {qx, qy} of window (q0, q1), then of (q0 + 1, q1) -- the same
 //                             bits as QS16's (k_prep_windows16)
 // ===================================================================================
@@ -168,13 +171,15 @@ __global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
         qs[o] = window_qs(s, s2, ws * ws, g.method);
     }
     Ss[idx] = dm_v4i{qs[0].x, qs[0].y, qs[1].x, qs[1].y};
-    const size_t tile = idx / 32; // (t, rp, q1 / 32): w0 % 32 == 0
+    // window q1 = 64 gq + 2 cc + j -> strip tile 2 gq + j, column cc (w0 % 64 == 0)
+    const size_t tile = (idx / w0) * (w0 / 32) + 2 * (q1 / 64) + (q1 & 1);
+    const int cc = (q1 % 64) >> 1;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         int w[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j >> 2] |= (pix[16 * h + j] & 0xFF) << (8 * (j & 3));
-        Bs[tile * 64 + (q1 % 32) + 32 * h] = dm_v4i{w[0], w[1], w[2], w[3]};
+        Bs[tile * 64 + cc + 32 * h] = dm_v4i{w[0], w[1], w[2], w[3]};
     }
 }
 
@@ -664,7 +669,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             (void *)(Bs + ((size_t)t * h2 * NT32 + 2 * wc) * 64), 0, 0x7fffffff, 0x00020000);
         const __amdgpu_buffer_rsrc_t rS2 = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(Ss + (size_t)t * h2 * w0 + 64 * wc), 0, 0x7fffffff, 0x00020000);
-        const unsigned voS = (unsigned)lane * 16u, voQ2 = (unsigned)c32 * 16u;
+        // (lane c32 of tile j: window 64 wc + 2 c32 + j, k_prep_strips)
+        const unsigned voS = (unsigned)lane * 16u, voQ2 = (unsigned)c32 * 32u;
         struct StripFrag {
             dm_v4i b[2], q[2];
         };
@@ -672,7 +678,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)(rp * NT32 + j) * 1024u, 0);
-                f.q[j] = __builtin_amdgcn_raw_buffer_load_b128(rS2, voQ2, (unsigned)(rp * w0 + 32 * j) * 16u, 0);
+                f.q[j] = __builtin_amdgcn_raw_buffer_load_b128(rS2, voQ2, (unsigned)(rp * w0 + j) * 16u, 0);
             }
         };
         const float nf = (float)n, nb = -nf * 12582912.0f; // y_of_acc's exact steps

@@ -14,6 +14,10 @@
 #           for 4 waves per SIMD, p = plain stores (DM_VL_F_*; results exact)
 #   s0      sweep 1 on the 16 x 16 tiles instead of the row-pair strips (DM_S1=0; results exact)
 #   x0      the level kernel's workgroups in dispatch order, not XCD-grouped (DM_XCD_MAP=0; exact)
+#   s2off   sweep 2 on the 16 x 16 tiles (k_level1_mfq) for every shape (DM_S2=0; results exact)
+#   s2all   the strip kernel (k_level12_strip) for C3 as well (DM_S2=7; results exact)
+#   c3mw3   the S = 128 strip kernel compiled for 3 waves per SIMD (A, patch sums in registers,
+#           two row pairs per loop trip; DM_C3_MW=3; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
 #   c5h2w4, c5f4m   the w0 = 256 volumes: binary16 min/max known with 2 x 512-B runs in
@@ -96,6 +100,9 @@ PY
     c2nb8) EXTRA="-DDM_C2_NB=8" ;;
     s0) EXTRA="-DDM_S1=0" ;;
     x0) EXTRA="-DDM_XCD_MAP=0" ;;
+    s2off) EXTRA="-DDM_S2=0" ;;
+    s2all) EXTRA="-DDM_S2=7" ;;
+    c3mw3) EXTRA="-DDM_S2=7 -DDM_C3_MW=3" ;;
     head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
           (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
              case $f in include/*) git show HEAD:$f > $r/$f ;; *) git show HEAD:$f > $d/csrc/$(basename $f) ;; esac; done) ;;

@@ -19,14 +19,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EM_AMDGPU = 224
 
 # The kernel instance each profiled shape launches depends on the library's compile-time
-# switches (dm_kernels.hip: DM_S1, DM_C*_NB, DM_VL_*), which the library reports through
+# switches (dm_kernels.hip: DM_S1, DM_S2, DM_C*_NB, DM_VL_*), which the library reports through
 # dm_build_config(); the symbols below are derived from it, so an A/B build made with -D
 # overrides (tools/abl_build.sh) is looked up under its own instances.  A library without
 # dm_build_config (before round 5) uses the round-4 instances (LEGACY).
 LEVEL = (64, 128, 256)       # profiled level-kernel tiles: C2, C3, C5
 VOLUME = ((128, 4, False), (128, 4, True), (128, 2, False), (128, 2, True),
           (256, 4, False), (256, 4, True), (256, 2, False), (256, 2, True))
-DEFAULTS = {'S1': 1, 'C2_NB': 4, 'C3_NB': 2, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
+DEFAULTS = {'S1': 1, 'S2': 0, 'XCD_MAP': 1, 'C2_NB': 4, 'C3_NB': 2, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
             'VL_H2_TR': 0, 'VL_H2_NW': 8, 'VL_F2_TR': 0, 'VL_F2_MW': 1, 'VL_HS_NW': 8, 'VL_F_NW': 8,
             'VL_F_TR': 4, 'VL_F_MW': 4, 'VL_F_NT': 1}
 LEGACY = {('level', 64): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',
@@ -72,8 +72,10 @@ def symbol(kind, tile, esz=None, mm=False, lib=None):
         if tile not in LEVEL:
             return None
         nb = c['C2_NB'] if tile == 64 else c['C3_NB'] if tile == 128 else c['C5_NB']
-        nw = nb * (1 if tile == 64 else 2 if tile == 128 else 4)
-        return 'k_level1_mfqILi1ELi4ELi%dELi4ELb1ELb1ELi%dELb1ELb%dEE' % (nw, nb, c['S1'])
+        nwc = 1 if tile == 64 else 2 if tile == 128 else 4
+        if (c['S2'] >> {64: 0, 128: 1, 256: 2}[tile]) & 1:   # both sweeps on the strips (dm_strip.h)
+            return 'k_level12_stripILi%dELi%dELb1ELb1ELi%dEE' % (nwc, nb, c.get('C3_MW', 4) if tile == 128 else 4)
+        return 'k_level1_mfqILi1ELi4ELi%dELi4ELb1ELb1ELi%dELb1ELb%dEE' % (nb * nwc, nb, c['S1'])
     if (tile, esz, bool(mm)) not in VOLUME:
         return None
     if tile == 128 and esz == 4:
