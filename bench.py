@@ -403,8 +403,9 @@ def level_roofline(solver, tile, l1_ms):
     valu_busy_pmc (SQ_ACTIVE_INST_VALU x 4 / (1024 x cycles)) prices every VALU instruction at
     4 cycles: an upper bound, kept for comparison with round 2."""
     mode = int(os.environ.get('DM_FUSE_L2', str(engine.FUSE_DEFAULT)))
-    kname = ('dm_corr_level1 (k_level1_mfq)' if mode == 0
-             else 'dm_corr_level12 (k_level1_mfq, level 2 fused)')
+    kern = 'k_level12_strip' if 'strip' in (kernel_hash.symbol('level', tile) or '') else 'k_level1_mfq'
+    kname = ('dm_corr_level1 (%s)' % kern if mode == 0
+             else 'dm_corr_level12 (%s, level 2 fused)' % kern)
     pmc = load_pmc(tile, 'level1', solver.batch.T)
     peak = 1024 * SPEC_CLOCK_GHZ
     roof = {'kernel': kname, 'bound': 'valu', 'ms': round(l1_ms, 3),

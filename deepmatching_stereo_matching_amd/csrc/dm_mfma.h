@@ -189,6 +189,9 @@ __global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
 // multiple of 8, workgroup b is given logical index (b % 8) * (grid / 8) + b / 8: each XCD then
 // walks one contiguous range of blocks, i.e. whole tiles in order, and the tile's window
 // operands stay in that XCD's L2 (placement only: any order is correct).
+#ifndef DM_LATE
+#define DM_LATE 1   // k_level1_mfq (L2F): the next even row's fragments loaded after the emission
+#endif
 #ifndef DM_XCD_MAP
 #define DM_XCD_MAP 1
 #endif
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
     __shared__ float4 cst[NB][4][6];   // [block][cell][field][child]: a_p, lo, hi, rmin, den, rinv
     // LATE: the next even row's fragments are loaded after the level-1 emission instead of
     // before it (12 fewer live VGPRs through the emission, less latency cover)
-    constexpr bool LATE = L2F;
+    constexpr bool LATE = L2F && DM_LATE;
     constexpr int L2V = 4 * GW, L2B = 64 / L2V; // level-2 values per wave per row; rows per stash
     // M == 1 (one pooled column per lane, valid on even lanes): the pooled children of RB
     // level-2 rows, [wave][row * 4 * L2V + child * L2V + column], rectified 64 at a time

@@ -14,6 +14,8 @@ import csv
 import glob
 import os
 
+LEVEL = ('k_level1_mfq', 'k_level12_strip')   # the level kernel (round 5: the strip form for S = 64, 256)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -28,7 +30,7 @@ def main():
                 name = r['Kernel_Name'].replace('void ', '').split('(')[0].split('<')[0]
                 rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), name))
     rows.sort()
-    lv = [r for r in rows if r[2] == 'k_level1_mfq']
+    lv = [r for r in rows if r[2] in LEVEL]
     timed = lv[args.warmup:args.warmup + args.steps + 1]
     t0, t1 = timed[0][0], timed[-1][0]          # steps periods, start to start
     n = len(timed) - 1
@@ -39,7 +41,7 @@ def main():
     outside = collections.Counter()
     calls = collections.Counter()
     for s, e, name in rows:
-        if name == 'k_level1_mfq' or e <= t0 or s >= t1:
+        if name in LEVEL or e <= t0 or s >= t1:
             continue
         s, e = max(s, t0), min(e, t1)
         ov = sum(max(0, min(e, b1) - max(s, b0)) for b0, b1 in busy)

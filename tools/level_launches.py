@@ -16,7 +16,7 @@ def main(root, bench, label):
     for path in kt:
         with open(path) as f:
             for r in csv.DictReader(f):
-                if r['Kernel_Name'].lstrip('void ').startswith('k_level1_mfq'):
+                if r['Kernel_Name'].lstrip('void ').startswith(('k_level1_mfq', 'k_level12_strip')):
                     rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0]))
     rows.sort()
     d = json.loads(open(bench).read().strip().splitlines()[-1])

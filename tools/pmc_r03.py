@@ -38,6 +38,9 @@ SHAPES = {  # shape -> (kernel prefix, f16 instantiation?, json name, tile, tile
 
 
 def _is(name, prefix):
+    if prefix == 'k_level1_mfq':   # the level kernel: k_level1_mfq or (round 5) k_level12_strip
+        return _is(name, 'k_level1_mfq_') or _is(name, 'k_level12_strip')
+    prefix = prefix.rstrip('_')
     if name.startswith('_Z'):
         return ('%d%sI' % (len(prefix), prefix)) in name[:len(prefix) + 8]
     return name.split('<')[0].split('(')[0].strip().split()[-1] == prefix

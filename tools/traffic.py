@@ -8,7 +8,7 @@ import os
 import sys
 
 # key: (kernel name prefixes, f16 instantiation?)
-KERNELS = {'level1': (('k_level1_mfq',), None), 'volume': (('k_volume_ls', 'k_volume_cs', 'k_volume_mfq'), False),
+KERNELS = {'level1': (('k_level1_mfq', 'k_level12_strip'), None), 'volume': (('k_volume_ls', 'k_volume_cs', 'k_volume_mfq'), False),
            'volume_f16': (('k_volume_ls', 'k_volume_cs'), True)}
 
 
