@@ -1,0 +1,56 @@
+"""Every profile bench.py reads at run time was made on the kernels of the in-tree build
+(VERDICT r4 next #7).
+
+bench.py prices the level kernel's live time with an issue-cycle model and reads HBM traffic,
+clock and profiled occupancy from committed PMC passes; it checks each file's recorded ISA hash
+against the library it loaded and reports null fields on a mismatch.  This CPU test turns a
+stale profile into a failing suite instead of a silent null on the driver's box: the hash of
+each profiled kernel instance (tools/kernel_hash.py, from the gfx950 code objects inside
+libdmstereo.so, instances derived from dm_build_config) must equal the hash the profile
+recorded.  Runs wherever the library is built (the driver's build() step builds it here)."""
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'tools'))
+import kernel_hash as K  # noqa: E402
+
+LIB = os.path.join(REPO, 'deepmatching_stereo_matching_amd', 'libdmstereo.so')
+LEVEL = {128: 'pmc_level1.json', 64: 'pmc_level1_s64.json', 256: 'pmc_level1_s256.json'}
+VOLUME = {(128, 4, False): 'pmc_volume.json', (128, 4, True): 'pmc_volume_mm.json',
+          (128, 2, False): 'pmc_volume_f16.json', (128, 2, True): 'pmc_volume_f16_mm.json',
+          (256, 4, False): 'pmc_volume_s256.json', (256, 4, True): 'pmc_volume_mm_s256.json',
+          (256, 2, False): 'pmc_volume_f16_s256.json', (256, 2, True): 'pmc_volume_f16_mm_s256.json'}
+
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason='libdmstereo.so not built')
+
+
+def _load(name):
+    with open(os.path.join(REPO, 'profiles', name)) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize('tile', sorted(LEVEL))
+def test_level_profiles_match_build(tile):
+    d = _load(LEVEL[tile])
+    cur = K.kernel_hash(K.symbol('level', tile, lib=LIB), LIB)
+    assert cur, 'profiled level-kernel instance not in the library'
+    assert d.get('isa_sha16') == cur, '%s: PMC pass made on ISA %s, the build holds %s' % (
+        LEVEL[tile], d.get('isa_sha16'), cur)
+    assert d.get('issue_model_isa_sha16') == cur, '%s: issue model made on ISA %s, the build holds %s' % (
+        LEVEL[tile], d.get('issue_model_isa_sha16'), cur)
+    # the model's instruction count was checked against the PMC pass of the same build
+    assert abs(d['issue_model_insts_vs_pmc'] - 1.0) < 0.03, d['issue_model_insts_vs_pmc']
+
+
+@pytest.mark.parametrize('key', sorted(VOLUME))
+def test_volume_profiles_match_build(key):
+    d = _load(VOLUME[key])
+    tile, esz, mm = key
+    cur = K.kernel_hash(K.symbol('volume', tile, esz, mm, lib=LIB), LIB)
+    assert cur, 'profiled volume-kernel instance not in the library'
+    assert d.get('isa_sha16') == cur, '%s: PMC pass made on ISA %s, the build holds %s' % (
+        VOLUME[key], d.get('isa_sha16'), cur)
