@@ -1592,11 +1592,18 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 #ifndef DM_VL_F_NT
 #define DM_VL_F_NT 1
 #endif
+// the min/max sweep of the volume kernels without a known min/max on the row-pair strips
+// dm_corr_stats leaves for the strip shapes (32 x 32 x 32 i8 MFMA, as the level kernel's sweep 1)
+#ifndef DM_VS1
+#define DM_VS1 1
+#endif
 template <typename OT>
 static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT *out, hipStream_t st,
                             int have_mm = 0)
 {
     if (!volume_ls_shape(b)) return DM_ERR_UNSUPPORTED;
+    dm_v4i *Bs = nullptr, *Ss = nullptr;
+    if (DM_VS1 && !have_mm && strip_shape(b)) strip_views(b, d_stats, &Bs, &Ss);
     const int G = b->w0 / 16, nw = 8;
     const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
     if (bpt % nw) return DM_ERR_UNSUPPORTED;
@@ -1617,14 +1624,14 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
                 constexpr int NWh = DM_VL_H_NW;
                 if (bpt % NWh) return DM_ERR_UNSUPPORTED;
                 k_volume_ls<8, NWh, DM_VL_H_NT, OT, DM_VL_H_TR><<<(unsigned)(b->T * bpt / NWh), 64 * NWh, 0, st>>>(
-                    gg, s, Bw, QS, out, have_mm);
+                    gg, s, Bw, QS, out, have_mm, Bs, Ss);
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
             if constexpr (DM_VL_HS_NW != 8) {
                 constexpr int NWs = DM_VL_HS_NW;
                 if (bpt % NWs) return DM_ERR_UNSUPPORTED;
-                k_volume_ls<8, NWs, true, OT><<<(unsigned)(b->T * bpt / NWs), 64 * NWs, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+                k_volume_ls<8, NWs, true, OT><<<(unsigned)(b->T * bpt / NWs), 64 * NWs, 0, st>>>(gg, s, Bw, QS, out, have_mm, Bs, Ss);
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
@@ -1632,7 +1639,7 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
             constexpr int NWf = DM_VL_F_NW;
             if (bpt % NWf) return DM_ERR_UNSUPPORTED;
             k_volume_ls<8, NWf, DM_VL_F_NT, OT, DM_VL_F_TR, DM_VL_F_MW><<<(unsigned)(b->T * bpt / NWf), 64 * NWf, 0, st>>>(
-                gg, s, Bw, QS, out, have_mm);
+                gg, s, Bw, QS, out, have_mm, Bs, Ss);
             HIP_TRY(hipGetLastError());
             return DM_OK;
         }
@@ -1643,17 +1650,17 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
                 constexpr int NWh = DM_VL_H2_NW;
                 if (bpt % NWh) return DM_ERR_UNSUPPORTED;
                 k_volume_ls<16, NWh, true, OT, DM_VL_H2_TR><<<(unsigned)(b->T * bpt / NWh), 64 * NWh, 0, st>>>(
-                    gg, s, Bw, QS, out, have_mm);
+                    gg, s, Bw, QS, out, have_mm, Bs, Ss);
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
         } else {
-            k_volume_ls<16, 8, true, OT, DM_VL_F2_TR, DM_VL_F2_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm);
+            k_volume_ls<16, 8, true, OT, DM_VL_F2_TR, DM_VL_F2_MW><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm, Bs, Ss);
             HIP_TRY(hipGetLastError());
             return DM_OK;
         }
     }
-#define DM_VL(G_) if (G == G_) { k_volume_ls<G_, 8, true, OT><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm); HIP_TRY(hipGetLastError()); return DM_OK; }
+#define DM_VL(G_) if (G == G_) { k_volume_ls<G_, 8, true, OT><<<grid, 64 * 8, 0, st>>>(gg, s, Bw, QS, out, have_mm, Bs, Ss); HIP_TRY(hipGetLastError()); return DM_OK; }
     DM_VL(2) DM_VL(4) DM_VL(8) DM_VL(16)
 #undef DM_VL
     return DM_ERR_UNSUPPORTED;
@@ -1687,7 +1694,7 @@ int dm_abi_version(void) { return 109; }
 #define DM_STR(x) DM_STR2(x)
 const char *dm_build_config(void)
 {
-    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C5_NB=" DM_STR(DM_C5_NB)
+    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " VS1=" DM_STR(DM_VS1) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C5_NB=" DM_STR(DM_C5_NB)
            " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
            " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
            " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_F_NW=" DM_STR(DM_VL_F_NW)

@@ -1190,7 +1190,9 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // ===================================================================================
 template <int G, int NW, bool NT, typename OT, int TR = 0, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
-                                                   const int2 *__restrict__ QS, OT *vol, int have_mm)
+                                                   const int2 *__restrict__ QS, OT *vol, int have_mm,
+                                                   const dm_v4i *__restrict__ Bs = nullptr,
+                                                   const dm_v4i *__restrict__ Ss = nullptr)
 {
     // have_mm: the per-patch rmin / rmax are already in the statistics workspace (written by
     // dm_corr_level1/12 or an earlier volume launch on the same stats): sweep 1 -- the MFMA,
@@ -1272,6 +1274,128 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
             clamp = clamp || (!cc && (ap[r] == 0.0f || rmx >= 1.0f || rmn[r] <= -1.0f));
         }
         clamp = __builtin_amdgcn_ballot_w64(clamp) != 0;
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (Bs) {
+        // ---- sweep 1 on the row-pair strips (dm_corr_stats' k_prep_strips, round 5): the
+        // 32 x 32 x 32 i8 MFMA gives this wave's 16 patches x 2 window rows x 32 windows per
+        // instruction (k_level1_mfq's strip sweep); the strips come from memory, so the LDS
+        // window rows are not needed until sweep 2 ----
+        const int c32 = lane & 31, hs = lane >> 5, h2 = h0 / 2;
+        constexpr int NT32 = W0 / 32, NGR = W0 >= 64 ? W0 / 64 : 1;   // strip tiles, 64-window groups per row pair
+        // A rows (lane & 31): patch lane & 15 shifted by ws taps for rows 16..31, K bytes 16 hs ..
+        dm_v4i A32;
+        {
+            const __amdgpu_buffer_rsrc_t rI = tile_rsrc(g.img1, g.pitch1, g, t);
+            const int pi = lane & 15, o = (lane >> 4) & 1, cl = pi >> 2, ch = pi & 3;
+            const int p0 = 2 * (I0 + (cl >> 1)) + (ch >> 1), p1 = 2 * (J0 + (cl & 1)) + (ch & 1);
+            const unsigned pb = (unsigned)(p0 * g.pitch1 + p1);
+            const int ws = g.ws;
+            int w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int bb = 0; bb < 16; ++bb) {
+                const int tau = 16 * hs + bb - ws * o;
+                const bool in = tau >= 0 && tau < n;
+                const int tc = tau < 0 ? 0 : (tau >= n ? n - 1 : tau);
+                const int v = (int)__builtin_amdgcn_raw_buffer_load_b8(rI, pb + (unsigned)((tc / ws) * g.pitch1 + tc % ws), 0, 0) - 128;
+                w[bb >> 2] |= ((in ? v : 0) & 0xFF) << (8 * (bb & 3));
+            }
+            A32 = dm_v4i{w[0], w[1], w[2], w[3]};
+        }
+        float sTs[8];   // [cell slot][child]: patch 4 (2 (k >> 2) + hs) + (k & 3)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int cell = 2 * (k >> 2) + hs, ch = k & 3;
+            const int p = (2 * (I0 + (cell >> 1)) + (ch >> 1)) * W0 + 2 * (J0 + (cell & 1)) + (ch & 1);
+            sTs[k] = (float)s.sT[tb + p];
+        }
+        const __amdgpu_buffer_rsrc_t rS1 =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(Bs + (size_t)t * h2 * NT32 * 64), 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rS2 =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(Ss + (size_t)t * h2 * W0), 0, 0x7fffffff, 0x00020000);
+        const unsigned voS = (unsigned)lane * 16u, voQ = (unsigned)c32 * 32u;
+        struct StripFrag {
+            dm_v4i b[2], q[2];
+        };
+        // unit k = (row pair k / NGR, 64-window group k % NGR): strip tiles 2 gr, 2 gr + 1
+        auto load_unit = [&](StripFrag &f, int k) {
+            const int rp = k / NGR, gr = k % NGR;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)(rp * NT32 + 2 * gr + j) * 1024u, 0);
+                f.q[j] = __builtin_amdgcn_raw_buffer_load_b128(rS2, voQ, (unsigned)(rp * W0 + 64 * gr + j) * 16u, 0);
+            }
+        };
+        const float nf = (float)n, nb = -nf * 12582912.0f; // y_of_acc's exact steps
+        const dm_v16i acc32 = {DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS,
+                               DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS, DM_YBIAS};
+        float mn8[8], mx8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { mn8[k] = INFINITY; mx8[k] = -INFINITY; }
+        const int NU = h2 * NGR;
+        // one fragment buffer, each part reloaded with unit k + 1's as soon as it is used (the
+        // volume kernels' sweep 2 keeps the registers of the 16 x 16 path)
+        auto minmax_unit = [&](StripFrag &f, int k) {
+            const int kn = __builtin_amdgcn_readfirstlane(k + 1 < NU ? k + 1 : k), rpn = kn / NGR, grn = kn % NGR;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const dm_v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A32, f.b[j], acc32, 0, 0, 0);
+                f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)(rpn * NT32 + 2 * grn + j) * 1024u, 0);
+                const dm_f2 qs0 = dm_f2{__int_as_float(f.q[j].x), __int_as_float(f.q[j].y)};
+                const dm_f2 qs1 = dm_f2{__int_as_float(f.q[j].z), __int_as_float(f.q[j].w)};
+                float y[16];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) { // register pair (2m, 2m + 1): window row m >> 2
+                    const int cs = (m >> 1) & 1, cp = m & 1;
+                    const dm_f2 qs = (m >> 2) ? qs1 : qs0;
+                    const dm_f2 a = dm_f2{__int_as_float(acc[2 * m]), __int_as_float(acc[2 * m + 1])};
+                    const dm_f2 mm = __builtin_elementwise_fma(a, dm_f2{nf, nf}, dm_f2{nb, nb});
+                    const dm_f2 nu = __builtin_elementwise_fma(dm_f2{sTs[4 * cs + 2 * cp], sTs[4 * cs + 2 * cp + 1]},
+                                                               __builtin_shufflevector(qs, qs, 0, 0), mm);
+                    const dm_f2 yy = pk_mul_bhi(qs, nu);
+                    y[2 * m] = yy.x; y[2 * m + 1] = yy.y;
+                }
+                f.q[j] = __builtin_amdgcn_raw_buffer_load_b128(rS2, voQ, (unsigned)(rpn * W0 + 64 * grn + j) * 16u, 0);
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                    mn8[kk] = fminf(fminf(mn8[kk], y[kk]), y[8 + kk]);
+                    mx8[kk] = fmaxf(fmaxf(mx8[kk], y[kk]), y[8 + kk]);
+                }
+            }
+        };
+        StripFrag fa;
+        load_unit(fa, 0);
+        for (int k = 0; k < NU; ++k) minmax_unit(fa, k);
+        half_wave_minmax(mn8, mx8);
+        // the 16 patches' extremes (lanes 31, 63) to the 16 x 16 layout (lane group = cell,
+        // accumulator row = child) through the LDS row buffer sweep 2 fills last
+        float *red = (float *)&lds[((h0 & 1) ^ 1) * BUF] + wave * 32;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int pl = 4 * (2 * (k >> 2) + hs) + (k & 3);
+            if (c32 == 31) { red[pl] = mn8[k]; red[16 + pl] = mx8[k]; }
+        }
+        fill(0, h0 & 1);   // sweep 2's row 0, in flight through the reduction
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float mnr = red[4 * grp + r], mxr = red[16 + 4 * grp + r];
+            rmn[r] = r_of_y(mnr, ap[r], g.method);
+            const float rmx = r_of_y(mxr, ap[r], g.method);
+            den[r] = __fsub_rn(rmx, rmn[r]);
+            rinv[r] = __frcp_rn(den[r]);
+            lo[r] = cc ? -INFINITY : (ap[r] == 0.0f ? 1.0f : -1.0f);
+            hi[r] = cc ? INFINITY : 1.0f;
+            clamp = clamp || (!cc && (ap[r] == 0.0f || __fmul_rn(mxr, ap[r]) > 1.0f ||
+                                      __fmul_rn(mnr, ap[r]) < -1.0f));
+            if (c == 0) {
+                const int p = (2 * Ic + (r >> 1)) * W0 + 2 * Jc + (r & 1);
+                s.rmn[tb + p] = rmn[r];
+                s.rmx[tb + p] = rmx;
+            }
+        }
+        clamp = __builtin_amdgcn_ballot_w64(clamp) != 0;   // wave-uniform
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
     fill(0, 0);

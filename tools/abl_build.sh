@@ -16,6 +16,7 @@
 #   x0      the level kernel's workgroups in dispatch order, not XCD-grouped (DM_XCD_MAP=0; exact)
 #   s2off   sweep 2 on the 16 x 16 tiles (k_level1_mfq) for every shape (DM_S2=0; results exact)
 #   s2all   the strip kernel (k_level12_strip) for C3 as well (DM_S2=7; results exact)
+#   vs0     the standalone volumes' min/max sweep on the 16 x 16 tiles, not the strips (DM_VS1=0; exact)
 #   c3mw3   the S = 128 strip kernel compiled for 3 waves per SIMD (A, patch sums in registers,
 #           two row pairs per loop trip; DM_C3_MW=3; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
@@ -103,6 +104,7 @@ PY
     s2off) EXTRA="-DDM_S2=0" ;;
     s2all) EXTRA="-DDM_S2=7" ;;
     c3mw3) EXTRA="-DDM_S2=7 -DDM_C3_MW=3" ;;
+    vs0) EXTRA="-DDM_VS1=0" ;;
     head) rm -rf $d/csrc $r/include; mkdir -p $d/csrc $r/include
           (cd $REPO && for f in $(git ls-files deepmatching_stereo_matching_amd/csrc include); do
              case $f in include/*) git show HEAD:$f > $r/$f ;; *) git show HEAD:$f > $d/csrc/$(basename $f) ;; esac; done) ;;
