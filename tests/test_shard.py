@@ -211,7 +211,7 @@ def _chunk_worker(rank, size, port, n, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('size,n,chunks', [(2, 256, 4), (3, 256, 4), (3, 10, 4), (2, 3, 2)])
+@pytest.mark.parametrize('size,n,chunks', [(2, 256, 4), (3, 256, 4), (3, 10, 4), (2, 3, 2), (8, 256, 4), (4, 3, 4)])
 def test_chunk_gather_bands(size, n, chunks):
     """ChunkGather (bands cut into chunks, one asynchronous gather per chunk) and the one-shot
     band gather deliver every unit to rank 0 in unit order; a gather over a size other than
