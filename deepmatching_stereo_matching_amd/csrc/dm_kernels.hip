@@ -1460,6 +1460,9 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 #ifndef DM_C5_NB
 #define DM_C5_NB 1   // four-wave cell blocks per workgroup of the S = 256 level kernel
 #endif
+#ifndef DM_C3_MINW
+#define DM_C3_MINW 4   // waves per SIMD k_level1_mfq's S = 128 instance is compiled for
+#endif
 #ifndef DM_C3_MW
 #define DM_C3_MW 4   // waves per SIMD the S = 128 strip kernel is compiled for
 #endif
@@ -1511,7 +1514,7 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
         if (Bs && (DM_S2 & 2)) k_level12_strip<2, NBc, L2F, CL, DM_C3_MW><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
-        else if (Bs) k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
+        else if (Bs) k_level1_mfq<1, 4, 2 * NBc, DM_C3_MINW, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
         return DM_OK;
