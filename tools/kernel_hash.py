@@ -75,7 +75,8 @@ def symbol(kind, tile, esz=None, mm=False, lib=None):
         nwc = 1 if tile == 64 else 2 if tile == 128 else 4
         if (c['S2'] >> {64: 0, 128: 1, 256: 2}[tile]) & 1:   # both sweeps on the strips (dm_strip.h)
             return 'k_level12_stripILi%dELi%dELb1ELb1ELi%dEE' % (nwc, nb, c.get('C3_MW', 4) if tile == 128 else 4)
-        return 'k_level1_mfqILi1ELi4ELi%dELi4ELb1ELb1ELi%dELb1ELb%dEE' % (nb * nwc, nb, c['S1'])
+        minw = c.get('C3_MINW', 4) if tile == 128 else 4
+        return 'k_level1_mfqILi1ELi4ELi%dELi%dELb1ELb1ELi%dELb1ELb%dEE' % (nb * nwc, minw, nb, c['S1'])
     if (tile, esz, bool(mm)) not in VOLUME:
         return None
     if tile == 128 and esz == 4:
