@@ -16,8 +16,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libdmstereo.so')
 SOURCES = [os.path.join(CSRC, 'dm_kernels.hip'), os.path.join(CSRC, 'dm_postproc.hip')]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ('dm_pow.h', 'dm_pow_tables.h', 'dm_mfma.h', 'dm_exp.h', 'dm_gs_pf.h')
-                  if os.path.exists(os.path.join(CSRC, f))] + \
+DEPS = SOURCES + sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')) + \
     [os.path.join(REPO, 'include', 'dmstereo.h')]
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')

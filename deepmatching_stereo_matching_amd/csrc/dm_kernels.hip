@@ -1583,6 +1583,9 @@ static int launch_mfq(const dm_tiles *b, void *d_stats, double *L1, double *L2, 
 #ifndef DM_VL_HS_NW
 #define DM_VL_HS_NW 8   // binary16 standalone (w0 = 128): waves per workgroup
 #endif
+#ifndef DM_VL_HS_TR
+#define DM_VL_HS_TR 0   // binary16 standalone (w0 = 128): 256-B chunks per store run (2 with 4 or 8
+#endif                  // waves: 8.24-8.29 against 8.04-8.10 ms, profiles/r05w_volume_ws_ab.txt)
 #ifndef DM_VL_F_NW
 #define DM_VL_F_NW 8    // float32 (w0 = 128): waves per workgroup
 #endif
@@ -1631,10 +1634,10 @@ static int launch_volume_ls(const dm_tiles *b, void *d_stats, const Stats &s, OT
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
-            if constexpr (DM_VL_HS_NW != 8) {
+            if constexpr (DM_VL_HS_NW != 8 || DM_VL_HS_TR != 0) {
                 constexpr int NWs = DM_VL_HS_NW;
                 if (bpt % NWs) return DM_ERR_UNSUPPORTED;
-                k_volume_ls<8, NWs, true, OT><<<(unsigned)(b->T * bpt / NWs), 64 * NWs, 0, st>>>(gg, s, Bw, QS, out, have_mm, Bs, Ss);
+                k_volume_ls<8, NWs, true, OT, DM_VL_HS_TR><<<(unsigned)(b->T * bpt / NWs), 64 * NWs, 0, st>>>(gg, s, Bw, QS, out, have_mm, Bs, Ss);
                 HIP_TRY(hipGetLastError());
                 return DM_OK;
             }
@@ -1700,7 +1703,7 @@ const char *dm_build_config(void)
     return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " VS1=" DM_STR(DM_VS1) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C3_MINW=" DM_STR(DM_C3_MINW) " C5_NB=" DM_STR(DM_C5_NB)
            " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
            " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
-           " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_F_NW=" DM_STR(DM_VL_F_NW)
+           " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_HS_TR=" DM_STR(DM_VL_HS_TR) " VL_F_NW=" DM_STR(DM_VL_F_NW)
            " VL_F_TR=" DM_STR(DM_VL_F_TR) " VL_F_MW=" DM_STR(DM_VL_F_MW) " VL_F_NT=" DM_STR(DM_VL_F_NT);
 }
 

@@ -21,6 +21,8 @@
 #           two row pairs per loop trip; DM_C3_MW=3; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
+#   hs4t2, hs8t2   the binary16 standalone volume in 4- / 8-wave workgroups with 2 x 512-B runs per
+#           store (DM_VL_HS_NW, DM_VL_HS_TR; results exact)
 #   c5h2w4, c5f4m   the w0 = 256 volumes: binary16 min/max known with 2 x 512-B runs in
 #           4-wave workgroups; float32 with 1-KB runs at 4 waves/SIMD (DM_VL_H2_*, DM_VL_F2_*)
 #   c2nb2, c2nb8   the S = 64 level kernel with 2 / 8 one-wave cell blocks per workgroup
@@ -79,6 +81,8 @@ s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
     ;;
+    hs4t2) EXTRA="-DDM_VL_HS_NW=4 -DDM_VL_HS_TR=2" ;;
+    hs8t2) EXTRA="-DDM_VL_HS_NW=8 -DDM_VL_HS_TR=2" ;;
     h2n) EXTRA="-DDM_VL_H_TR=2" ;;
     h2p) EXTRA="-DDM_VL_H_TR=2 -DDM_VL_H_NT=0" ;;
     h4p) EXTRA="-DDM_VL_H_TR=4 -DDM_VL_H_NT=0" ;;
