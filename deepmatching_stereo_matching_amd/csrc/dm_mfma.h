@@ -1188,6 +1188,13 @@ __global__ __launch_bounds__(256) void k_volume_mfq(Geo g, Stats s, const dm_v4i
 // run per store instruction, no LDS stage.
 // Arithmetic per voxel is k_volume_mfq's (same y, r, Markstein x): bit-identical output.
 // ===================================================================================
+// the standalone volumes' strip min/max sweep with each unit staged in LDS once per workgroup (1)
+// or read from L2 by every wave (0).  Same box, bit-identical (profiles/r05x_vs1lds_ab.txt):
+// C3 float32 13.58/13.56 -> 12.64/12.70 ms, C5-size binary16 16.00/16.13 -> 15.78/15.79,
+// C3 binary16 and C5-size float32 within 0.4 %
+#ifndef DM_VS1_LDS
+#define DM_VS1_LDS 1
+#endif
 template <int G, int NW, bool NT, typename OT, int TR = 0, int MW = 1, int GW = (16 / (int)sizeof(OT)) < G ? (16 / (int)sizeof(OT)) : G>
 __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const dm_v4i *__restrict__ Bw,
                                                    const int2 *__restrict__ QS, OT *vol, int have_mm,
@@ -1362,9 +1369,59 @@ __global__ __launch_bounds__(64 * NW, MW) void k_volume_ls(Geo g, Stats s, const
                 }
             }
         };
-        StripFrag fa;
-        load_unit(fa, 0);
-        for (int k = 0; k < NU; ++k) minmax_unit(fa, k);
+        if constexpr (DM_VS1_LDS && BUF >= 4096) {
+            // the workgroup's waves sweep the same units: each unit's 2 strip tiles (2 KB) and
+            // window stats (1 KB) come into LDS once per workgroup by LDS-DMA (instruction i by
+            // wave i % NW), double-buffered in the row buffers, one barrier per unit
+            constexpr int STG = 4096;
+            auto stage = [&](int k, int sb) {
+                const int rp = k / NGR, gr = k % NGR;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (i % NW != wave) continue;
+                    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)(sb * STG + i * 1024));
+                    if (i < 2) lds_dma16(rS1, dst, voS, (unsigned)(rp * NT32 + 2 * gr + i) * 1024u);
+                    else lds_dma16(rS2, dst, voS, (unsigned)(rp * W0 + 64 * gr) * 16u);
+                }
+            };
+            stage(0, 0);
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            for (int k = 0; k < NU; ++k) {
+                const int sb = k & 1;
+                if (k + 1 < NU) stage(k + 1, sb ^ 1);
+                const char *u = &lds[sb * STG];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const dm_v4i bj = *(const dm_v4i *)(u + j * 1024 + lane * 16);
+                    const dm_v4i qj = *(const dm_v4i *)(u + 2048 + c32 * 32 + j * 16);
+                    const dm_v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A32, bj, acc32, 0, 0, 0);
+                    const dm_f2 qs0 = dm_f2{__int_as_float(qj.x), __int_as_float(qj.y)};
+                    const dm_f2 qs1 = dm_f2{__int_as_float(qj.z), __int_as_float(qj.w)};
+                    float y[16];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) {
+                        const int cs = (m >> 1) & 1, cp = m & 1;
+                        const dm_f2 qs = (m >> 2) ? qs1 : qs0;
+                        const dm_f2 a = dm_f2{__int_as_float(acc[2 * m]), __int_as_float(acc[2 * m + 1])};
+                        const dm_f2 mm = __builtin_elementwise_fma(a, dm_f2{nf, nf}, dm_f2{nb, nb});
+                        const dm_f2 nu = __builtin_elementwise_fma(dm_f2{sTs[4 * cs + 2 * cp], sTs[4 * cs + 2 * cp + 1]},
+                                                                   __builtin_shufflevector(qs, qs, 0, 0), mm);
+                        const dm_f2 yy = pk_mul_bhi(qs, nu);
+                        y[2 * m] = yy.x; y[2 * m + 1] = yy.y;
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk) {
+                        mn8[kk] = fminf(fminf(mn8[kk], y[kk]), y[8 + kk]);
+                        mx8[kk] = fmaxf(fmaxf(mx8[kk], y[kk]), y[8 + kk]);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+        } else {
+            StripFrag fa;
+            load_unit(fa, 0);
+            for (int k = 0; k < NU; ++k) minmax_unit(fa, k);
+        }
         half_wave_minmax(mn8, mx8);
         // the 16 patches' extremes (lanes 31, 63) to the 16 x 16 layout (lane group = cell,
         // accumulator row = child) through the LDS row buffer sweep 2 fills last

@@ -127,10 +127,29 @@ def _symbols(data, base):
     return out
 
 
+def _mask_pc_literals(code):
+    """The code with the 32-bit literals of `s_getpc_b64` + `s_add_u32` / `s_addc_u32` zeroed:
+    those are the PC-relative offsets of the constant tables (the pow tables' rel32 relocations),
+    which move whenever another kernel of the library grows -- not part of this kernel's ISA.
+    gfx9 encodings: s_getpc_b64 = SOP1 0xBE80_1C00 | sdst << 16; the adds are SOP2 (bits 31:30 =
+    0b10) with ssrc1 = 0xFF, the literal in the next word."""
+    n = len(code) // 4
+    w = list(struct.unpack_from('<%dI' % n, code))
+    for i in range(n):
+        if (w[i] & 0xFF80FF00) != 0xBE801C00:
+            continue
+        j = i + 1
+        for _ in range(2):
+            if j + 1 < n and (w[j] >> 30) == 2 and ((w[j] >> 8) & 0xFF) == 0xFF:
+                w[j + 1] = 0
+                j += 2
+    return struct.pack('<%dI' % n, *w) + code[4 * n:]
+
+
 def kernel_hash(symbol_substring, lib=None):
-    """sha256 (hex, 16 chars) of the machine code + kernel descriptor (less its code offset) of
-    the ONE kernel whose mangled name contains `symbol_substring`; None if the library or the
-    kernel is absent."""
+    """sha256 (hex, 16 chars) of the machine code (PC-relative table offsets masked,
+    _mask_pc_literals) + kernel descriptor (less its code offset) of the ONE kernel whose
+    mangled name contains `symbol_substring`; None if the library or the kernel is absent."""
     lib = _lib_path(lib)
     try:
         data = open(lib, 'rb').read()
@@ -142,7 +161,7 @@ def kernel_hash(symbol_substring, lib=None):
         for nm, (off, size) in syms.items():
             if symbol_substring in nm and not nm.endswith('.kd') and size:
                 kd = syms.get(nm + '.kd')
-                h = hashlib.sha256(data[off:off + size])
+                h = hashlib.sha256(_mask_pc_literals(data[off:off + size]))
                 if kd:
                     # the descriptor without kernel_code_entry_byte_offset (bytes 16-23): that
                     # field is where the linker put the code relative to the descriptor, which
