@@ -21,6 +21,9 @@
 #           two row pairs per loop trip; DM_C3_MW=3; results exact)
 #   head    the last commit's sources (an A/B of the working tree against it)
 #   hsw4, fw4   the w0 = 128 binary16 standalone / float32 volumes in 4-wave workgroups
+#   smilp, smclause, strack   every kernel scheduled by the AMDGPU machine scheduler's max-ilp /
+#           max-memory-clause strategy, or with the AMDGPU register-pressure trackers (-mllvm
+#           -amdgpu-sched-strategy=..., -amdgpu-use-amdgpu-trackers; results exact: scheduling only)
 #   vs1l2   the standalone volumes' strip min/max sweep with every wave reading the units from
 #           L2 instead of each unit staged in LDS once per workgroup (DM_VS1_LDS=0; exact)
 #   hs4t2, hs8t2   the binary16 standalone volume in 4- / 8-wave workgroups with 2 x 512-B runs per
@@ -83,6 +86,9 @@ s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
     ;;
+    smilp) EXTRA="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
+    smclause) EXTRA="-mllvm -amdgpu-sched-strategy=max-memory-clause" ;;
+    strack) EXTRA="-mllvm -amdgpu-use-amdgpu-trackers" ;;
     vs1l2) EXTRA="-DDM_VS1_LDS=0" ;;
     hs4t2) EXTRA="-DDM_VL_HS_NW=4 -DDM_VL_HS_TR=2" ;;
     hs8t2) EXTRA="-DDM_VL_HS_NW=8 -DDM_VL_HS_TR=2" ;;
