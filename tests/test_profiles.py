@@ -25,7 +25,7 @@ VOLUME = {(128, 4, False): 'pmc_volume.json', (128, 4, True): 'pmc_volume_mm.jso
           (256, 4, False): 'pmc_volume_s256.json', (256, 4, True): 'pmc_volume_mm_s256.json',
           (256, 2, False): 'pmc_volume_f16_s256.json', (256, 2, True): 'pmc_volume_f16_mm_s256.json'}
 
-pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason='libdmstereo.so not built')
+_needs_lib = pytest.mark.skipif(not os.path.exists(LIB), reason="libdmstereo.so not built")
 
 
 def _load(name):
@@ -33,6 +33,7 @@ def _load(name):
         return json.load(f)
 
 
+@_needs_lib
 @pytest.mark.parametrize('tile', sorted(LEVEL))
 def test_level_profiles_match_build(tile):
     d = _load(LEVEL[tile])
@@ -46,6 +47,7 @@ def test_level_profiles_match_build(tile):
     assert abs(d['issue_model_insts_vs_pmc'] - 1.0) < 0.03, d['issue_model_insts_vs_pmc']
 
 
+@_needs_lib
 @pytest.mark.parametrize('key', sorted(VOLUME))
 def test_volume_profiles_match_build(key):
     d = _load(VOLUME[key])
@@ -54,3 +56,20 @@ def test_volume_profiles_match_build(key):
     assert cur, 'profiled volume-kernel instance not in the library'
     assert d.get('isa_sha16') == cur, '%s: PMC pass made on ISA %s, the build holds %s' % (
         VOLUME[key], d.get('isa_sha16'), cur)
+
+
+def test_hash_masks_pc_relative_table_offsets():
+    """The ISA hash ignores the literals of s_getpc_b64 + s_add_u32 / s_addc_u32 (the constant
+    tables' PC-relative offsets, which move when another kernel grows) and nothing else."""
+    import struct
+    getpc, add, addc = 0xBE861C00, 0x8006FF06, 0x8207FF07   # s_getpc_b64 s[6:7]; s_add(c)_u32 s6/s7, lit
+    other = 0xD2080002
+    a = struct.pack('<7I', getpc, add, 0xFFF62910, addc, 0xFFFFFFFF, other, 0x12345678)
+    b = struct.pack('<7I', getpc, add, 0x00001234, addc, 0x00000000, other, 0x12345678)
+    c = struct.pack('<7I', getpc, add, 0x00001234, addc, 0x00000000, other, 0x12345679)
+    assert K._mask_pc_literals(a) == K._mask_pc_literals(b)
+    assert K._mask_pc_literals(b) != K._mask_pc_literals(c)
+    # a literal after an add that does not follow s_getpc stays part of the hash
+    d = struct.pack('<3I', add, 0x1, other)
+    e = struct.pack('<3I', add, 0x2, other)
+    assert K._mask_pc_literals(d) != K._mask_pc_literals(e)
