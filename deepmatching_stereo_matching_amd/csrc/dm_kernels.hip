@@ -1486,7 +1486,7 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     if (KS == 1 && GW == 4 && NW == 4) {
         constexpr int NBc = DM_C5_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
-        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        if (bpt % NBc) return fail(DM_ERR_UNSUPPORTED, "cell blocks per tile not a multiple of %d (fill_ptab: a workgroup in one tile)", NBc);
         if (Bs && (DM_S2 & 4)) k_level12_strip<4, NBc, L2F, CL, 4><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
         else if (Bs) k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 4 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 4 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
@@ -1500,7 +1500,7 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     if (KS == 1 && GW == 4 && NW == 1) {
         constexpr int NBc = DM_C2_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
-        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        if (bpt % NBc) return fail(DM_ERR_UNSUPPORTED, "cell blocks per tile not a multiple of %d (fill_ptab: a workgroup in one tile)", NBc);
         if (Bs && (DM_S2 & 1)) k_level12_strip<1, NBc, L2F, CL, 4><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
         else if (Bs) k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
@@ -1512,7 +1512,7 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
     if (KS == 1 && GW == 4 && NW == 2) {
         constexpr int NBc = DM_C3_NB;
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
-        if (((size_t)b->T * bpt) % NBc) return fail(DM_ERR_UNSUPPORTED, "cell-block count not a multiple of %d", NBc);
+        if (bpt % NBc) return fail(DM_ERR_UNSUPPORTED, "cell blocks per tile not a multiple of %d (fill_ptab: a workgroup in one tile)", NBc);
         if (Bs && (DM_S2 & 2)) k_level12_strip<2, NBc, L2F, CL, DM_C3_MW><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
         else if (Bs) k_level1_mfq<1, 4, 2 * NBc, DM_C3_MINW, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);

@@ -246,10 +246,16 @@ __device__ __forceinline__ void fill_ptab(unsigned (&ptab)[NB][16][16], const Ge
 // issued for all 2N values before the next step, so no instruction reads a VGPR the one just
 // before it wrote (the DPP read-after-VALU-write hazard needs 2 wait states); the values are
 // never NaN.  (Five DPP instructions per value instead of five ds_bpermute shuffles.)
+// N >= 2 keeps a value's DPP read >= 3 instructions after its write inside the sequence.  The
+// compiler cannot see DPP inside asm, so tests/test_profiles.py checks the built ISA: no VALU
+// write of a VGPR within the 2 wait states before a DPP read of it, in every kernel of the
+// library (__builtin_amdgcn_update_dpp + fminf is not folded into v_min_f32_dpp --
+// fminf's canonicalising v_max x, x sits between -- and costs 256 VALU instructions per wave,
+// and one asm block over all 16 values changes the register allocation into a spill).
 template <int N>
 __device__ __forceinline__ void half_wave_minmax(float (&mn)[N], float (&mx)[N])
 {
-    static_assert(N >= 1, "");
+    static_assert(N >= 2, "a value's next DPP read must come >= 2 wait states after its write");
 #define DM_HWR(ctl, rm)                                                                                   \
     _Pragma("unroll") for (int k = 0; k < N; ++k) {                                                       \
         asm volatile("v_min_f32_dpp %0, %0, %0 " ctl " row_mask:" rm " bank_mask:0xf" : "+v"(mn[k]));      \

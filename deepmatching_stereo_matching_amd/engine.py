@@ -413,6 +413,8 @@ def subpix_map_tiles(pyr, match, stream=None):
         raise ValueError('match must be a contiguous float64 [T][3][h][w] tensor (T = %d)' % b.T)
     if not pyr._have_minmax:   # the per-patch min / max a level kernel or volume leaves in the stats
         pyr.build(nlev=2)
+    if stream is not None and pyr.stream is not None and stream != pyr.stream:
+        stream.wait_stream(pyr.stream)   # the stats the pyramid's stream wrote
     _, _, hm, wm = m.shape
     L.check(pyr.lib.dm_subpix_map_tiles(b.ref(), L.ptr(pyr.stats), hm, wm, L.ptr(m),
                                         L.stream_handle(stream) if stream is not None else pyr._s()),

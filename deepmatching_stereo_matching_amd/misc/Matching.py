@@ -98,6 +98,9 @@ class Matching():
                             self.filtering_mode, nlev=n)[0]
         elif isinstance(pyr, engine.DevicePyramid):
             levels = [lst.device(k).reshape(pyr.level_shape(k)) for k in range(bottom, n)]
+            # match_levels runs on the current stream: it reads levels the pyramid wrote on its own
+            if pyr.stream is not None:
+                torch.cuda.current_stream().wait_stream(pyr.stream)
             out = engine.match_levels(levels, sub_here, self.filtering, self.filter_window_size,
                                       fnum, self.filtering_mode)
         else:
@@ -105,7 +108,9 @@ class Matching():
                                       self.filter_window_size, fnum, self.filtering_mode)
         if self.sub_pix and bottom > 0:
             if isinstance(pyr, engine.DevicePyramid):
-                engine.subpix_map_tiles(pyr, out)
+                # the stream match_levels wrote `out` on (the pyramid's own stream
+                # would refine the map before dm_match has written it)
+                engine.subpix_map_tiles(pyr, out, stream=torch.cuda.current_stream())
             else:
                 engine.subpix_map(lst[0], out)
         if self.filtering:  # _initial_move_map / _B decrement it once per level (:91-93, :136-138)

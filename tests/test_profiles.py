@@ -73,3 +73,106 @@ def test_hash_masks_pc_relative_table_offsets():
     d = struct.pack('<3I', add, 0x1, other)
     e = struct.pack('<3I', add, 0x2, other)
     assert K._mask_pc_literals(d) != K._mask_pc_literals(e)
+
+
+def _profiles_with_symbols():
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', '*.json'))):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+
+        def walk(x, path):
+            if isinstance(x, dict):
+                if isinstance(x.get('kernel'), str) and x.get('isa_symbol'):
+                    out.append((path, x['kernel'], x['isa_symbol']))
+                for k, v in x.items():
+                    walk(v, path + '/' + k)
+        walk(d, os.path.basename(f))
+    return out
+
+
+@pytest.mark.parametrize('path,label,sym', _profiles_with_symbols())
+def test_profile_label_names_the_profiled_kernel(path, label, sym):
+    """A profile's "kernel" label is the kernel its isa_symbol names (the
+    strip kernel's passes were labelled k_level1_mfq)."""
+    assert label.split(' ')[0] == sym.split('I', 1)[0], (path, label, sym)
+
+
+def _vregs(tok):
+    """VGPR numbers named by one operand token ('v7', 'v[2:3]'), else ()."""
+    import re
+    m = re.match(r'^v(\d+)$', tok) or re.match(r'^v\[(\d+):(\d+)\]$', tok)
+    if not m:
+        return ()
+    lo = int(m.group(1))
+    hi = int(m.group(2)) if m.lastindex == 2 else lo
+    return tuple(range(lo, hi + 1))
+
+
+def dpp_hazards(disasm_lines):
+    """(function, line) of every DPP instruction whose DPP source VGPR was written by a VALU
+    instruction within the 2 wait states before it (gfx9: VALU write VGPR -> DPP read of it needs
+    2; s_nop n supplies n + 1), scanning each function's instructions in order."""
+    import re
+    bad, fn, recent = [], None, []   # recent: the written-VGPR sets of the last wait-state slots
+    for ln in disasm_lines:
+        if re.match(r'^[0-9a-f]+ <.*>:$', ln.strip()):
+            fn, recent = ln.strip(), []
+            continue
+        s = ln.split('//')[0].strip()
+        if not s or s.endswith(':'):
+            continue
+        op, _, rest = s.partition(' ')
+        ops = [t.strip() for t in rest.split(',')] if rest else []
+        if '_dpp' in op and len(ops) >= 2:
+            src = set(_vregs(ops[1].split()[0]))
+            if any(src & w for w in recent[-2:]):
+                bad.append((fn, s))
+        if op == 's_nop':
+            recent.extend([set()] * (int(ops[0], 0) + 1) if ops else [set()])
+        elif op.startswith('v_') and not op.startswith(('v_cmp', 'v_readlane', 'v_readfirstlane')) and ops:
+            recent.append(set(_vregs(ops[0])))
+        else:
+            recent.append(set())
+        recent = recent[-2:]
+    return bad
+
+
+def test_dpp_hazard_checker_itself():
+    ok = ['0000 <k>:', 'v_add_f32_e32 v5, v1, v2', 's_nop 1',
+          'v_min_f32_dpp v5, v5, v5 row_ror:8 row_mask:0xf bank_mask:0xf']
+    bad = ['0000 <k>:', 'v_add_f32_e32 v5, v1, v2', 'v_mov_b32_e32 v6, v1',
+           'v_min_f32_dpp v5, v5, v5 row_ror:8 row_mask:0xf bank_mask:0xf']
+    wide = ['0000 <k>:', 'v_pk_mul_f32 v[4:5], v[0:1], v[2:3]', 's_nop 0',
+            'v_max_f32_dpp v5, v5, v5 row_ror:8 row_mask:0xf bank_mask:0xf']
+    assert dpp_hazards(ok) == [] and len(dpp_hazards(bad)) == 1 and len(dpp_hazards(wide)) == 1
+
+
+@_needs_lib
+def test_no_dpp_read_after_valu_write_hazard_in_library(tmp_path):
+    """half_wave_minmax issues DPP min/max from inline asm, which the compiler's hazard
+    recognizer cannot see; its s_nop and the instruction order inside the sequence are what keep
+    a DPP read >= 2 wait states after the VALU write of its operand.  The check runs over the
+    built gfx950 code, every kernel, so a register copy the compiler places in between fails it."""
+    import shutil
+    import struct
+    import subprocess
+    objdump = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+    if not os.path.exists(objdump):
+        pytest.skip('llvm-objdump not available')
+    data = open(LIB, 'rb').read()
+    n_dpp = 0
+    for i, base in enumerate(K._elfs(data)):
+        shoff, = struct.unpack_from('<Q', data, base + 0x28)
+        shentsize, shnum = struct.unpack_from('<HH', data, base + 0x3A)
+        co = tmp_path / ('co%d.elf' % i)
+        co.write_bytes(data[base:base + shoff + shnum * shentsize])
+        out = subprocess.run([objdump, '-d', '--no-show-raw-insn', str(co)], capture_output=True,
+                             text=True, check=True).stdout.splitlines()
+        n_dpp += sum('_dpp' in ln for ln in out)
+        bad = dpp_hazards(out)
+        assert not bad, bad[:5]
+    assert n_dpp > 0

@@ -26,9 +26,13 @@ EM_AMDGPU = 224
 LEVEL = (64, 128, 256)       # profiled level-kernel tiles: C2, C3, C5
 VOLUME = ((128, 4, False), (128, 4, True), (128, 2, False), (128, 2, True),
           (256, 4, False), (256, 4, True), (256, 2, False), (256, 2, True))
-DEFAULTS = {'S1': 1, 'S2': 0, 'XCD_MAP': 1, 'C2_NB': 4, 'C3_NB': 2, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
-            'VL_H2_TR': 0, 'VL_H2_NW': 8, 'VL_F2_TR': 0, 'VL_F2_MW': 1, 'VL_HS_NW': 8, 'VL_F_NW': 8,
-            'VL_F_TR': 4, 'VL_F_MW': 4, 'VL_F_NT': 1}
+# DEFAULTS mirror the C defaults of dm_kernels.hip (every key dm_build_config reports); they
+# only fill keys a library's config string lacks -- a library that cannot be loaded at all is
+# an error (symbol() raises), never a guess.
+DEFAULTS = {'S1': 1, 'S2': 5, 'VS1': 1, 'VS1_LDS': 1, 'XCD_MAP': 1, 'C2_NB': 4, 'C3_NB': 2, 'C3_MW': 4,
+            'C3_MINW': 4, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
+            'VL_H2_TR': 0, 'VL_H2_NW': 8, 'VL_F2_TR': 0, 'VL_F2_MW': 1, 'VL_HS_NW': 8, 'VL_HS_TR': 0,
+            'VL_F_NW': 8, 'VL_F_TR': 4, 'VL_F_MW': 4, 'VL_F_NT': 1}
 LEGACY = {('level', 64): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi4ELb1EE',
           ('level', 128): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi2ELb1EE',
           ('level', 256): 'k_level1_mfqILi1ELi4ELi4ELi4ELb1ELb1ELi1ELb1EE'}
@@ -65,17 +69,19 @@ def symbol(kind, tile, esz=None, mm=False, lib=None):
     bytes per voxel, min/max known or not) that a tile of side `tile` launches in `lib` (the
     loaded one by default); None if not profiled."""
     cfg = build_config(lib)
+    if cfg is None:
+        raise RuntimeError('kernel_hash.symbol: cannot load %s to read its build config' % _lib_path(lib))
     if cfg == {} and kind == 'level':
         return LEGACY.get((kind, tile))
-    c = dict(DEFAULTS, **(cfg or {}))
+    c = dict(DEFAULTS, **cfg)
     if kind == 'level':
         if tile not in LEVEL:
             return None
         nb = c['C2_NB'] if tile == 64 else c['C3_NB'] if tile == 128 else c['C5_NB']
         nwc = 1 if tile == 64 else 2 if tile == 128 else 4
         if (c['S2'] >> {64: 0, 128: 1, 256: 2}[tile]) & 1:   # both sweeps on the strips (dm_strip.h)
-            return 'k_level12_stripILi%dELi%dELb1ELb1ELi%dEE' % (nwc, nb, c.get('C3_MW', 4) if tile == 128 else 4)
-        minw = c.get('C3_MINW', 4) if tile == 128 else 4
+            return 'k_level12_stripILi%dELi%dELb1ELb1ELi%dEE' % (nwc, nb, c['C3_MW'] if tile == 128 else 4)
+        minw = c['C3_MINW'] if tile == 128 else 4
         return 'k_level1_mfqILi1ELi4ELi%dELi%dELb1ELb1ELi%dELb1ELb%dEE' % (nb * nwc, minw, nb, c['S1'])
     if (tile, esz, bool(mm)) not in VOLUME:
         return None
@@ -84,7 +90,7 @@ def symbol(kind, tile, esz=None, mm=False, lib=None):
     if tile == 128:
         if mm:
             return 'k_volume_lsILi8ELi%dELb%dEDF16_Li%dELi1E' % (c['VL_H_NW'], c['VL_H_NT'], c['VL_H_TR'])
-        return 'k_volume_lsILi8ELi%dELb1EDF16_Li0ELi1E' % c['VL_HS_NW']
+        return 'k_volume_lsILi8ELi%dELb1EDF16_Li%dELi1E' % (c['VL_HS_NW'], c['VL_HS_TR'])
     if esz == 4:
         return 'k_volume_lsILi16ELi8ELb1EfLi%dELi%dE' % (c['VL_F2_TR'], c['VL_F2_MW'])
     if mm:

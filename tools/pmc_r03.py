@@ -80,6 +80,12 @@ def launches(d, prefix, f16, skip_first=False):
     return {k: (t, cnt[k]) for k, t in dur.items() if t >= 0.5 * big and k in cnt}
 
 
+def kernel_label(sym):
+    """The kernel's name (the template prefix of its mangled-name fragment), e.g.
+    'k_level12_stripILi1E...' -> 'k_level12_strip'."""
+    return sym.split('I', 1)[0] if 'I' in sym else sym
+
+
 def mean(ls, counter):
     v = [c[counter] for _, c in ls.values() if counter in c]
     return sum(v) / len(v) if v else None
@@ -94,12 +100,14 @@ def main(root):
         wr = launches(os.path.join(root, shape + '_write'), prefix, f16, mm)
         if not sq and not fe:
             continue
-        d = {'kernel': prefix + (' (binary16)' if f16 else ''), 'tile': tile, 'tiles': tiles,
+        sym = (kernel_hash.symbol('level', tile) if prefix == 'k_level1_mfq'
+               else kernel_hash.symbol('volume', tile, 2 if f16 else 4, mm))
+        # the label names the instance the pass profiled (k_level1_mfq or k_level12_strip)
+        label = kernel_label(sym) if sym else prefix
+        d = {'kernel': label + (' (binary16)' if f16 else ''), 'tile': tile, 'tiles': tiles,
              'source': 'tools/pmc_r03.sh %s (rocprofv3 --kernel-trace --pmc, separate passes)' % shape}
         # the ISA these counters were taken on (the library the passes loaded): bench.py uses
         # the figures only while its loaded library holds the same kernel bytes
-        sym = (kernel_hash.symbol('level', tile) if prefix == 'k_level1_mfq'
-               else kernel_hash.symbol('volume', tile, 2 if f16 else 4, mm))
         d['isa_symbol'] = sym
         d['isa_sha16'] = kernel_hash.kernel_hash(sym) if sym else None
         if sq:
