@@ -122,12 +122,11 @@ class PairSolver:
     dominant kernel (dm_corr_level12)."""
 
     def __init__(self, img1, img2, tile, grid, split=False, levels=None, chunks=None):
-        """split: the pair's tiles are sharded over the ranks of the process group (rank r
-        solves one contiguous band of tiles, shard.rank_band) and the per-tile results are
-        gathered to rank 0 (RCCL over xGMI), which stitches the map; the band is solved in
-        `chunks` chunks, each chunk's gather issued as soon as it is computed so it overlaps
-        the next chunk (shard.ChunkGather).  Otherwise this rank solves every tile of its own
-        pair in one batch.  levels: k-level pyramid (None: the full pyramid)."""
+        """split: the pair's tiles are sharded over the ranks of the process group by
+        shard.BandSolver -- the product path of ImageCutSolver's tile sharding (rank r solves one
+        contiguous band of tiles in `chunks` chunks, each chunk's results gathered to rank 0
+        behind the compute; rank 0 stitches the map).  Otherwise this rank solves every tile of
+        its own pair in one batch.  levels: k-level pyramid (None: the full pyramid)."""
         from deepmatching_stereo_matching_amd import shard
         self.dev = img1.device
         self.tile = tile
@@ -135,25 +134,21 @@ class PairSolver:
         self.n, origins = engine.cut_grid(tuple(img1.shape), [tile, tile], [tile, tile], WS)
         assert self.n == [grid, grid], self.n
         self.split = bool(split)
-        self.nchunks = chunks
-        self.rank, self.world = shard.world() if split else (0, 1)
         self.T = len(origins)
         if self.split:
-            g = self._gather()
-            self.chunk_idx = [g.chunk_units(c) for c in range(g.chunks)]
-            self.origins = origins[shard.rank_band(self.T, self.rank, self.world)]
+            self.band = shard.BandSolver(img1, img2, origins, tile, tile, WS, L.DM_TM_CCOEFF_NORMED,
+                                         device=self.dev, chunks=chunks or C5_CHUNKS, dst=0)
+            self.rank, self.world = self.band.rank, self.band.size
+            self.chunk_idx = self.band.chunk_idx
+            self.batches = self.band.batches
+            self.origins = origins[self.band.tiles()]
         else:
+            self.rank, self.world = 0, 1
             self.chunk_idx = [list(range(self.T))]
             self.origins = origins
-        self.batches = [engine.TileBatch(img1, img2, origins[idx], tile, tile, WS, L.DM_TM_CCOEFF_NORMED, self.dev)
-                        if idx else None for idx in self.chunk_idx]
+            self.batches = [engine.TileBatch(img1, img2, origins, tile, tile, WS, L.DM_TM_CCOEFF_NORMED, self.dev)]
         self.batch = next((b for b in self.batches if b is not None), None)
         self.ev = []        # per timed solve: [(start, end) of each chunk's level kernel]
-
-    def _gather(self):
-        from deepmatching_stereo_matching_amd import shard
-        return shard.ChunkGather(self.T, self.rank, self.world, (3, self.tile, self.tile), torch.float64,
-                                 self.dev, dst=0, chunks=self.nchunks or C5_CHUNKS)
 
     def step(self, timed=False, stream=None, wait=None, level_stream=None, stats_stream=None):
         """One full solve of the pair on `stream` (default: the current stream).  Every
@@ -166,9 +161,8 @@ class PairSolver:
                 return self.step(timed=timed, wait=wait, level_stream=level_stream,
                                  stats_stream=stats_stream)
         if self.split:   # rank 0 receives every tile's (3, S, S) result and stitches
-            g = self._gather()
-            self.compute(timed=timed, wait=wait, level_stream=level_stream, stats_stream=stats_stream, gather=g)
-            match = g.result()
+            match = self.start_split(timed=timed, wait=wait, level_stream=level_stream,
+                                     stats_stream=stats_stream).result()
             if match is None:
                 return None
         else:
@@ -177,31 +171,34 @@ class PairSolver:
         return engine.stitch(match, self.n, self.tile, self.tile, [self.tile, self.tile],
                              ['elevation'])
 
-    def compute(self, timed=False, wait=None, level_stream=None, stats_stream=None, gather=None):
-        """This rank's tiles, chunk by chunk: stats, dm_corr_level12 [timed], dm_aggregate
-        levels 3.., matching with sub-pixel -> float64 [T_chunk][3][S][S] on the current
-        stream; with `gather` each chunk's result is handed to it (put) as soon as it is
-        issued, else the one chunk's result is returned."""
-        evs, out = [], None
-        for c, b in enumerate(self.batches):
-            if b is None:   # a rank with fewer tiles than the others: an empty chunk
-                out = torch.empty((0, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
-            else:
-                pyr = engine.DevicePyramid(b, build=False, stats_stream=stats_stream)
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                evs.append(ev)
-                self.last_end = ev[1]
-                diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
-                pyr.build(events=ev, wait=wait if c == 0 else None,
-                          nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
-                if diag:
-                    out = torch.zeros((b.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
-                else:
-                    out = pyr.match(sub_pix=True, nlev=self.levels)
-            if gather is not None:
-                gather.put(c, out)
+    def start_split(self, timed=False, wait=None, level_stream=None, stats_stream=None):
+        """The split solve's band on the current stream through shard.BandSolver.start (each
+        chunk's gather issued behind it) -> its ChunkGather; the chunks' level-kernel events
+        are kept for level1_ms when timed."""
+        evs = []
+        g = self.band.start(sub_pix=True, nlev=self.levels, events=evs, wait=wait,
+                            level_stream=level_stream, stats_stream=stats_stream)
+        if evs:
+            self.last_end = evs[-1][1]
         if timed:
             self.ev.append(evs)
+        return g
+
+    def compute(self, timed=False, wait=None, level_stream=None, stats_stream=None):
+        """This rank's whole pair in one batch: stats, dm_corr_level12 [timed], dm_aggregate
+        levels 3.., matching with sub-pixel -> float64 [T][3][S][S] on the current stream."""
+        b = self.batch
+        pyr = engine.DevicePyramid(b, build=False, stats_stream=stats_stream)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        self.last_end = ev[1]
+        diag = os.environ.get('DM_BENCH_DIAG', '')   # tools only: 'nomatch' / 'l12only' (not a bench line)
+        pyr.build(events=ev, wait=wait, nlev=3 if diag == 'l12only' else self.levels, level_stream=level_stream)
+        if diag:
+            out = torch.zeros((b.T, 3, self.tile, self.tile), dtype=torch.float64, device=self.dev)
+        else:
+            out = pyr.match(sub_pix=True, nlev=self.levels)
+        if timed:
+            self.ev.append([ev])
         return out
 
     def level1_ms(self):
@@ -445,7 +442,50 @@ def level_roofline(solver, tile, l1_ms):
         if k in pmc:
             roof[k] = pmc[k]
     roof['traffic'] = pmc.get('hbm_bytes_per_launch')
+    work = level_work(pmc, solver.batch.T, tile)
+    if work:
+        roof['work'] = work
     return roof
+
+
+# float64 pow evaluations per level-0 voxel: the reference rectifies every value of levels 0, 1
+# and 2 (misc/Correlation_map.py:141,148: V + V/16 + V/256); the fused kernel pools before it
+# rectifies (pow14 is monotone): 4 child pows per level-1 value (V/4), one
+# per pooled level-1 value of each level-2 window and cell (V/64) and one per level-2 value (V/256)
+POW_REF_PER_VOXEL = 1.0 + 1.0 / 16 + 1.0 / 256
+POW_POOLED_PER_VOXEL = 1.0 / 4 + 1.0 / 64 + 1.0 / 256
+FMA_F64_PER_POW = 7    # pow14_zf / pow14_core_r: five series steps, fma(Phi, q, Plo), fma(Phi, G, s)
+
+
+def level_work(pmc, T, tile):
+    """roofline.work: the work the level kernel EXECUTES against the work
+    the algorithm needs, from the PMC work pass of the same ISA (profiles/pmc_level1*.json,
+    tools/pmc_r03.sh 'work'), so that a change which removes redundant work shows as less work
+    and not only as a different issue-slot fraction.
+      mac_slots_vs_algorithmic: i8 MFMA multiply-adds executed (SQ_INSTS_VALU_MFMA_MOPS_I8 x 512
+        math ops / 2) over ws^2 = 25 per level-0 voxel (each voxel's correlation once); sweep 1
+        (min / max) and sweep 2 (pooling) each compute every voxel, and K = 32 holds 25 or 30 taps.
+      pow_evals_per_voxel: float64 FMAs executed (SQ_INSTS_VALU_FMA_F64 wave instructions x 64
+        lanes) / 7 per pow evaluation, over V; beside it the reference's count (every value of
+        levels 0-2) and the pool-before-rectify count (pow14 is monotone: only pooled values).
+    None without a work pass made on this ISA (the caller drops it with the PMC pass)."""
+    w = pmc.get('work_counters_per_launch') if pmc else None
+    if not w or not w.get('SQ_INSTS_VALU_MFMA_MOPS_I8'):
+        return None
+    V = T * float(tile) ** 4
+    macs = w['SQ_INSTS_VALU_MFMA_MOPS_I8'] * 512 / 2.0
+    pows = w.get('SQ_INSTS_VALU_FMA_F64', 0.0) * 64 / FMA_F64_PER_POW
+    return {'voxels_per_launch': V,
+            'mac_slots_per_launch': macs, 'macs_algorithmic_per_launch': WS * WS * V,
+            'mac_slots_vs_algorithmic': round(macs / (WS * WS * V), 4),
+            'pow_evals_per_launch': pows, 'pow_evals_per_voxel': round(pows / V, 5),
+            'pow_evals_reference_per_voxel': round(POW_REF_PER_VOXEL, 5),
+            'pow_evals_pool_before_rectify_per_voxel': round(POW_POOLED_PER_VOXEL, 5),
+            'pow_evals_vs_reference': round(pows / V / POW_REF_PER_VOXEL, 4),
+            'f64_insts_per_launch': {k: w.get(k) for k in ('SQ_INSTS_VALU_FMA_F64', 'SQ_INSTS_VALU_MUL_F64',
+                                                           'SQ_INSTS_VALU_ADD_F64')},
+            'source': 'profile: PMC work pass (tools/pmc_r03.sh work) of this ISA; MACs = MOPS_I8 x 512 / 2, '
+                      'pows = FMA_F64 x 64 lanes / %d' % FMA_F64_PER_POW}
 
 
 def volume_equivalent(solver, tile, l1_ms):
@@ -469,8 +509,7 @@ def split_breakdown(solver, rank, world, dev):
     torch.cuda.synchronize()
     tdist.barrier()
     t0 = time.perf_counter()
-    g = solver._gather()
-    solver.compute(gather=g)
+    g = solver.start_split()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     full = g.result()
@@ -650,14 +689,19 @@ def c5_split(args, rank, world, dev, dist):
     import torch.distributed as tdist
     tile, grid = CONFIGS['c5']
     side = (grid + 1) * tile + WS - 1
-    a, b = stereo_pair(side, side, seed=1000, dx=2, max_disp=tile // 4, sinusoidal=True)
-    img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    # the pair is made (read, for a real input) on rank 0 only and sent to every rank once
+    # (shard.broadcast_pair: 2 x 19 MB of uint8, before the timed region)
+    from deepmatching_stereo_matching_amd import shard
+    a = b = None
+    if rank == 0 or not shard._group():
+        a, b = stereo_pair(side, side, seed=1000, dx=2, max_disp=tile // 4, sinusoidal=True)
+    img1, img2 = shard.broadcast_pair(a, b, src=0, device=dev)
     del a, b
     voxels = grid * grid * float(tile) ** 4
     steps, warmup = args.c5_steps, 1
     # with a process group (N > 1, or the one-rank RCCL group main() starts at N = 1) the tiles
-    # go through the split path: bands, chunked gathers to rank 0
-    from deepmatching_stereo_matching_amd import shard
+    # go through the split path: shard.BandSolver, the product path of ImageCutSolver's tile
+    # sharding (bands, chunked gathers to rank 0)
     split = world > 1 or shard.world()[1] == 1 and shard._group()
     solver = PairSolver(img1, img2, tile, grid, split=split)
     pipe = Pipeline([solver], dev, dist, nstreams=max(1, args.streams), chain_levels=args.chain_levels)

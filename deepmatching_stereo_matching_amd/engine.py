@@ -449,16 +449,27 @@ def cut_grid(shape, image_size, stride, window_size):
     return n, np.array(org, dtype=np.int64)
 
 
-def tile_bytes(h0, w0):
-    """Device bytes one tile needs inside DevicePyramid + match (levels >= 1, stats, maps)."""
+def tile_bytes(h0, w0, level1=True):
+    """Device bytes one tile needs inside DevicePyramid + match (levels >= 1, stats, maps).
+    ``level1=False``: without the float64 level 1, which the fused level kernel never stores
+    (DM_FUSE_L2=2, the default: matching re-derives it) -- 2.1 GB of the 2.3 GB of an S = 256
+    tile."""
     nlev, _ = pyramid_plan(h0, w0)
     P = h0 * w0
     total = 6 * 4 * P + 2 * 3 * 8 * P
     h, w = h0, w0
-    for _ in range(1, nlev):
+    for k in range(1, nlev):
         h, w = h // 2, w // 2
-        total += 8 * (h * w) ** 2
+        if k > 1 or level1:
+            total += 8 * (h * w) ** 2
     return total
+
+
+def level1_stored():
+    """Does a DevicePyramid of the current configuration store level 1 (DM_FUSE_L2 != 2)?  The
+    fused level kernel (mode 2) keeps it on chip; a shape it does not take stores it anyway, so
+    callers sizing memory for such shapes keep tile_bytes' default."""
+    return int(os.environ.get('DM_FUSE_L2', str(FUSE_DEFAULT))) != 2
 
 
 def _on(stream):

@@ -112,9 +112,12 @@ class ImageCutSolver():
         """All tiles in batches on the GPU -> (d_map, out_map) device tensors.  The tile grid
         is self.len, counted on the image shape BEFORE _padding (:46,58-62).  Opted in to tile
         sharding (shard.tile_sharding() or DM_SHARD_TILES=1) under a torch.distributed process
-        group, the tiles are sharded over its ranks (shard.solve_tiles_sharded: rank r solves
-        tiles r::N, results all-gathered) and every rank stitches the whole map; every rank
-        must then solve the same pair."""
+        group, the tiles are sharded over its ranks by shard.BandSolver -- the path bench.py's
+        c5_split line measures: rank r solves one contiguous band of tiles in chunks, each
+        chunk's results gathered to rank 0 behind the compute, rank 0 stitches -- and the maps
+        come back on every rank (one broadcast; tile_sharding(result='root'): rank 0 only, the
+        others get None).  Every rank must then solve the same pair (shard.broadcast_pair
+        sends it from rank 0)."""
         from deepmatching_stereo_matching_amd import shard
         n = list(self.len)
         if n[0] < 1 or n[1] < 1:
@@ -127,9 +130,12 @@ class ImageCutSolver():
                 L.METHODS[self.feature_name], self.sub_pix, self.filtering,
                 self.filtering_window_size, self.filtering_num, self.filtering_mode)
         if shard.tile_sharding_enabled():
-            match = shard.solve_tiles_sharded(*args)
-        else:
-            match = engine.solve_tiles(*args)
+            return shard.solve_image_sharded(self.img1, self.img2, [h0, w0], self.stride, self.window_size,
+                                             L.METHODS[self.feature_name], self.degree_map_mode,
+                                             self.sub_pix, self.filtering, self.filtering_window_size,
+                                             self.filtering_num, self.filtering_mode,
+                                             result=shard.shard_result(), grid=(n, origins))
+        match = engine.solve_tiles(*args)
         return engine.stitch(match, n, h0, w0, self.stride, self.degree_map_mode)
 
     def _execute_matching(self):
@@ -137,8 +143,9 @@ class ImageCutSolver():
         小画像ごとにマッチングを行い結果を結合
         """
         d_map, out_map = self._execute_matching_device()
-        self.d_map = d_map.cpu().numpy()
-        self.out_map = out_map.cpu().numpy()
+        # (None on the ranks other than 0 of a sharded solve with tile_sharding(result='root'))
+        self.d_map = d_map.cpu().numpy() if d_map is not None else None
+        self.out_map = out_map.cpu().numpy() if out_map is not None else None
 
     def __call__(self):
         self._cut_and_pool()

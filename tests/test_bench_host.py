@@ -89,3 +89,33 @@ def test_store_ceiling_follows_the_instance_pattern(bench):
     assert '"volx_nt"' in f['source'] and '"vol_nt"' in c5['source']
     assert h_mm['frac'] == round(5000.0 / h_mm['gb_s'], 4)
     assert bench.store_ceiling(64, 64, 2, 5000.0) is None
+
+
+def test_roofline_work_derivation(bench, monkeypatch):
+    """roofline.work: MAC slots from the PMC MFMA math-op counter and pow
+    evaluations from the float64 FMA count, each against the algorithmic count; present only
+    with a work pass made on the loaded ISA."""
+    import kernel_hash as K
+    cur = K.kernel_hash(K.symbol('level', 128))
+    V = 64 * 128.0 ** 4
+    # round 5's C3 launch: 16.8 M 32x32x32 + 67.1 M 16x16x32 i8 MFMAs = 1.0995 T multiply-adds;
+    # 4 child pows per level-1 value (V/4) + V/64 + V/256 pooled ones, 7 float64 FMAs each
+    macs = 16777216 * 32768 + 67108864 * 8192
+    pows = V * (0.25 + 1 / 64.0 + 1 / 256.0)
+    work = {'SQ_INSTS_VALU_MFMA_MOPS_I8': macs * 2 / 512.0, 'SQ_INSTS_VALU_FMA_F64': pows * 7 / 64.0,
+            'SQ_INSTS_VALU_MUL_F64': 1.0, 'SQ_INSTS_VALU_ADD_F64': 2.0}
+    good = {'tile': 128, 'tiles': 64, 'issue_cycles_per_launch': 12.25e9, 'gpu_cycles_per_launch': 13.5e6,
+            'issue_model_isa_sha16': cur, 'isa_sha16': cur, 'work_counters_per_launch': work}
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: dict(good))
+    w = bench.level_roofline(_Solver(), 128, 7.0)['work']
+    assert w['mac_slots_per_launch'] == pytest.approx(macs)
+    assert w['mac_slots_vs_algorithmic'] == pytest.approx(macs / (25 * V), abs=1e-4)
+    assert w['mac_slots_vs_algorithmic'] == pytest.approx(2.56, abs=0.01)
+    assert w['pow_evals_per_voxel'] == pytest.approx(0.25 + 1 / 64.0 + 1 / 256.0, abs=1e-5)
+    assert w['pow_evals_vs_reference'] == pytest.approx(w['pow_evals_per_voxel'] / (1 + 1 / 16.0 + 1 / 256.0), abs=1e-4)
+    # no work pass, or a work pass of other kernel bytes: no work object
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: {k_: v for k_, v in good.items()
+                                                             if k_ != 'work_counters_per_launch'})
+    assert 'work' not in bench.level_roofline(_Solver(), 128, 7.0)
+    monkeypatch.setattr(bench, 'load_pmc', lambda *a, **k: dict(good, isa_sha16='0123456789abcdef'))
+    assert 'work' not in bench.level_roofline(_Solver(), 128, 7.0)

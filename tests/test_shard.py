@@ -133,6 +133,7 @@ def _patch_engine():
         return torch.from_numpy(d), torch.from_numpy(s)
     engine.solve_tiles = _oracle_tiles
     engine.stitch = stitch
+    shard.TILE_SOLVER = _oracle_tiles     # BandSolver's chunks (the sharded ImageCutSolver)
 
 
 def test_pairs_sharded_with_image_cut_solver_unequal_counts():
@@ -144,6 +145,7 @@ def test_pairs_sharded_with_image_cut_solver_unequal_counts():
                for a, b in _pairs()]
     finally:
         engine.solve_tiles, engine.stitch = ref_engine
+        shard.TILE_SOLVER = None
     size = 3
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
@@ -243,3 +245,100 @@ def test_chunk_gather_without_group():
     assert torch.equal(g.result(), torch.arange(5, dtype=torch.float64).reshape(5, 1))
     with pytest.raises(ValueError):
         shard.gather_units_to(torch.zeros((2, 1)), 4, 0, 2)
+
+
+def _band_worker(rank, size, port, q):
+    """The product path of a tiled pair on every rank: the pair sent from rank
+    0 (broadcast_pair), ImageCutSolver with tile sharding -> shard.BandSolver (bands, chunked
+    gathers to rank 0, rank 0 stitches) with the maps returned on every rank ('all') or on rank
+    0 only ('root'), and BandSolver itself (the object bench.py's c5_split drives)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=size)
+    try:
+        _patch_engine()
+        from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+        a, b = _case() if rank == 0 else (None, None)
+        i1, i2 = shard.broadcast_pair(a, b, src=0, device='cpu')
+        a, b = i1.numpy(), i2.numpy()
+        with shard.tile_sharding():
+            all_ = ImageCutSolver(a, b, image_size=[16, 16], stride=[12, 16], window_size=5,
+                                  degree_map_mode=['elevation', 'distance'])()
+        with shard.tile_sharding(result='root'):
+            root = ImageCutSolver(a, b, image_size=[16, 16], stride=[12, 16], window_size=5,
+                                  degree_map_mode=['elevation', 'distance'])()
+        n, org = engine.cut_grid(a.shape, [16, 16], [12, 16], 5)
+        band = shard.BandSolver(a, b, org, 16, 16, 5, 5, chunks=2)
+        m = band.solve()
+        q.put((rank, (a, b), all_, root, None if m is None else m.numpy(), band.tiles(),
+               len(band.chunk_idx)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('size', [2, 3])
+def test_band_solver_through_image_cut_solver(size):
+    ref_engine = (engine.solve_tiles, engine.stitch)
+    try:
+        _patch_engine()
+        from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+        a, b = _case()
+        ref = ImageCutSolver(a, b, image_size=[16, 16], stride=[12, 16], window_size=5,
+                             degree_map_mode=['elevation', 'distance'])()
+        n, org = engine.cut_grid(a.shape, [16, 16], [12, 16], 5)
+        ref_m = _oracle_tiles(a, b, org, 16, 16, 5, 5, True, False, 3, 3, 'median').numpy()
+    finally:
+        engine.solve_tiles, engine.stitch = ref_engine
+        shard.TILE_SOLVER = None
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(size)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T = len(org)
+    tiles = []
+    for rank, pair, all_, root, m, mine, nch in res:
+        assert np.array_equal(pair[0], a) and np.array_equal(pair[1], b)   # broadcast_pair
+        assert np.array_equal(all_[0], ref[0], equal_nan=True) and np.array_equal(all_[1], ref[1], equal_nan=True)
+        if rank == 0:
+            assert np.array_equal(root[0], ref[0], equal_nan=True) and np.array_equal(root[1], ref[1], equal_nan=True)
+            assert np.array_equal(m, ref_m, equal_nan=True)
+        else:
+            assert root == (None, None) and m is None
+        assert mine == shard.rank_band(T, rank, size)
+        tiles += mine
+        assert nch == res[0][6]          # every rank issues the same number of gathers
+    assert tiles == list(range(T))
+
+
+def test_band_solver_single_process_and_result_setting(monkeypatch):
+    """Without a process group BandSolver solves every tile (the chunks only bound memory), and a
+    memory budget below one chunk's pyramid raises the chunk count; shard_result() follows
+    tile_sharding(result=) and DM_SHARD_RESULT."""
+    a, b = _case()
+    n, org = engine.cut_grid(a.shape, [16, 16], [12, 16], 5)
+    band = shard.BandSolver(a, b, org, 16, 16, 5, 5, chunks=2, solver=_oracle_tiles)
+    assert band.tiles() == list(range(len(org))) and len(band.chunk_idx) == 2
+    m = band.solve()
+    assert np.array_equal(m.numpy(), _oracle_tiles(a, b, org, 16, 16, 5, 5, True, False, 3, 3, 'median').numpy(),
+                          equal_nan=True)
+    small = shard.BandSolver(a, b, org, 16, 16, 5, 5, chunks=1, solver=_oracle_tiles,
+                             mem_budget=engine.tile_bytes(16, 16) * 3)
+    assert len(small.chunk_idx) == -(-len(org) // 3)
+    monkeypatch.delenv('DM_SHARD_RESULT', raising=False)
+    assert shard.shard_result() == 'all'
+    with shard.tile_sharding(result='root'):
+        assert shard.shard_result() == 'root'
+        with shard.tile_sharding():
+            assert shard.shard_result() == 'root'
+    monkeypatch.setenv('DM_SHARD_RESULT', 'root')
+    assert shard.shard_result() == 'root'
+    with pytest.raises(ValueError):
+        with shard.tile_sharding(result='some'):
+            pass
+    i1, i2 = shard.broadcast_pair(a, b, device='cpu')
+    assert np.array_equal(i1.numpy(), a) and np.array_equal(i2.numpy(), b)

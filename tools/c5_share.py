@@ -1,18 +1,19 @@
 """C5 strong-scaling forecast from one GPU (diagnostic; never a bench line).
 
-bench.py --config c5 --gpus N shards one 4096^2 pair's 256 tiles round-robin over N ranks
-(rank r solves tiles r::N), gathers each rank's (3, S, S) float64 results to rank 0 over
-RCCL and rank 0 stitches the map (bench.py PairSolver.step, shard.gather_units_to).  The
-driver measures N = 1..8 on an 8-GPU node; this tool measures on ONE GPU the parts that
-decide the curve:
-  - rank 0's share: the same pipelined solve (2 HIP streams, as bench.py) of tiles 0::N,
-    timed over --steps steps after --warmup, for N = 1, 2, 4, 8;
+bench.py's c5_split line (and ImageCutSolver's tile sharding) solve one 4096^2 pair's 256 tiles
+with shard.BandSolver: rank r takes one contiguous band of T/N tiles (shard.rank_band), solves
+it in 4 chunks (DM_C5_CHUNKS), and each chunk's (3, S, S) float64 results go to rank 0 by an
+asynchronous RCCL gather issued behind it; rank 0 stitches.  The driver measures N = 1..8 on an
+8-GPU node; this tool measures on ONE GPU the parts that decide the curve:
+  - rank 0's band: the same BandSolver (4 chunks, 2 HIP streams pipelined as bench.py) over
+    tiles rank_band(256, 0, N), timed over --steps steps after --warmup, N = 1, 2, 4, 8;
   - rank 0's stitch of the whole map from the gathered (256, 3, S, S) results;
-  - the gather itself is priced, not measured (one GPU has no xGMI peer): every peer sends
-    its T/N tiles x 3 x S^2 x 8 B over its own link, at --link-gbs (default 50 GB/s, a third
-    of the 153 GB/s per-link figure of MI355X_MICROARCH.md, so a pessimistic price).
-forecast speed-up(N) = t(1) / (t_share(N) + t_stitch + t_gather(N)), where t(1) is the
-one-rank step (which stitches too and gathers nothing).
+  - the gather is priced, not measured (one GPU has no xGMI peer): every peer sends its band
+    chunk by chunk over its own link at --link-gbs (default 50 GB/s, a third of the 153 GB/s
+    per-link figure of MI355X_MICROARCH.md: a pessimistic price); chunks 0..2 travel while the
+    band's later chunks compute, so only the LAST chunk's transfer is exposed.
+forecast speed-up(N) = t(1) / (t_band(N) + t_last_chunk_gather(N) + t_stitch), t(1) the one-rank
+step (which stitches too and gathers nothing).
 
   python3 tools/c5_share.py [--steps 6 --warmup 2] > gpurun_out/c5_share.json
 """
@@ -31,13 +32,15 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 from deepmatching_stereo_matching_amd import engine  # noqa: E402
 from deepmatching_stereo_matching_amd import _lib as L  # noqa: E402
+from deepmatching_stereo_matching_amd import shard  # noqa: E402
 from deepmatching_stereo_matching_amd.synthetic import stereo_pair  # noqa: E402
 
 
-def timed_steps(solver, steps, warmup, stitch):
-    """bench.py's pipelined loop for one solver: consecutive solves alternate over two
-    streams, each solve's level kernel waits for the previous one's.  stitch: the solve ends
-    in engine.stitch of this share (N = 1: the whole map, as bench.py's one-rank step)."""
+def timed_steps(band, steps, warmup, stitch, n, tile):
+    """bench.py's pipelined loop for one BandSolver: consecutive solves alternate over two
+    streams, each solve's first level kernel waits for the previous solve's last one.  stitch:
+    the solve ends in engine.stitch of the assembled map (N = 1: the whole pair, as bench.py's
+    one-rank step)."""
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     prev = [None]
     k = [0]
@@ -46,11 +49,12 @@ def timed_steps(solver, steps, warmup, stitch):
         st = streams[k[0] % 2]
         k[0] += 1
         with torch.cuda.stream(st):
-            m = solver.compute(wait=prev[0])
-            prev[0] = solver.last_end
+            evs = []
+            g = band.start(sub_pix=True, events=evs, wait=prev[0])
+            prev[0] = evs[-1][1]
+            m = g.result()
             if stitch:
-                engine.stitch(m, solver.n, solver.tile, solver.tile, [solver.tile, solver.tile],
-                              ['elevation'])
+                engine.stitch(m, n, tile, tile, [tile, tile], ['elevation'])
 
     for _ in range(warmup):
         one()
@@ -68,6 +72,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--ranks', default='1,2,4,8')
     ap.add_argument('--link-gbs', type=float, default=50.0)
+    ap.add_argument('--chunks', type=int, default=bench.C5_CHUNKS)
     args = ap.parse_args()
     tile, grid = bench.CONFIGS['c5']
     side = (grid + 1) * tile + bench.WS - 1
@@ -76,10 +81,12 @@ def main():
     img1, img2 = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
     full = bench.PairSolver(img1, img2, tile, grid)
     all_origins = full.origins
+    full_n = full.n
     T = len(all_origins)
-    out = {'what': 'C5 strong-scaling forecast from one GPU (tools/c5_share.py): rank 0 share '
-                   'measured, gather priced, stitch measured; diagnostic, not a bench line',
-           'tiles': T, 'tile': tile, 'steps': args.steps, 'warmup': args.warmup,
+    out = {'what': 'C5 strong-scaling forecast from one GPU (tools/c5_share.py): rank 0\'s band through '
+                   'shard.BandSolver (%d chunks) measured, chunked gather priced (last chunk exposed), '
+                   'stitch measured; diagnostic, not a bench line' % args.chunks,
+           'tiles': T, 'tile': tile, 'steps': args.steps, 'warmup': args.warmup, 'chunks': args.chunks,
            'link_gbs_assumed': args.link_gbs, 'shares': []}
 
     # rank 0's stitch of the whole map from the gathered results
@@ -94,31 +101,36 @@ def main():
             ts.append((time.perf_counter() - t0) * 1e3)
     t_stitch = sum(ts) / len(ts)
     out['stitch_full_ms'] = round(t_stitch, 3)
-    del m
+    del m, full
+    torch.cuda.empty_cache()
 
     t1 = None
     for n in [int(x) for x in args.ranks.split(',')]:
-        s = bench.PairSolver(img1, img2, tile, grid)
-        s.origins = all_origins[0::n]
-        s.T = T
-        s.batch = engine.TileBatch(img1, img2, s.origins, tile, tile, bench.WS,
-                                   L.DM_TM_CCOEFF_NORMED, dev)
-        ms = timed_steps(s, args.steps, args.warmup, stitch=(n == 1))
-        rec = {'ranks': n, 'rank0_tiles': len(s.origins), 'rank0_solve_ms': round(ms, 3)}
+        mine = shard.rank_band(T, 0, n)
+        band = shard.BandSolver(img1, img2, all_origins[mine], tile, tile, bench.WS, L.DM_TM_CCOEFF_NORMED,
+                                device=dev, chunks=args.chunks)
+        ms = timed_steps(band, args.steps, args.warmup, n == 1, full_n, tile)
+        chunk_tiles = [len(c) for c in band.chunk_idx]
+        rec = {'ranks': n, 'rank0_tiles': len(mine), 'rank0_band': [mine[0], mine[-1]],
+               'chunk_tiles': chunk_tiles, 'rank0_solve_ms': round(ms, 3)}
         if n == 1:
             t1 = ms
             rec['step_ms'] = round(ms, 3)
         else:
-            peer_bytes = len(s.origins) * 3 * tile * tile * 8
-            t_gather = peer_bytes / (args.link_gbs * 1e9) * 1e3
-            step = ms + t_gather + t_stitch
-            rec.update({'gather_bytes_per_peer': peer_bytes, 'gather_ms_priced': round(t_gather, 3),
+            tb = 3 * tile * tile * 8
+            peer_bytes = len(mine) * tb
+            t_gather_all = peer_bytes / (args.link_gbs * 1e9) * 1e3
+            t_gather_last = chunk_tiles[-1] * tb / (args.link_gbs * 1e9) * 1e3
+            step = ms + t_gather_last + t_stitch
+            rec.update({'gather_bytes_per_peer': peer_bytes, 'gather_bytes_per_chunk': chunk_tiles[-1] * tb,
+                        'gather_ms_priced_whole_band': round(t_gather_all, 3),
+                        'gather_ms_priced_exposed': round(t_gather_last, 3),
                         'step_ms_forecast': round(step, 3),
                         'speedup_forecast': round(t1 / step, 3) if t1 else None,
                         'share_efficiency': round(t1 / (n * ms), 4) if t1 else None})
         out['shares'].append(rec)
         print(json.dumps(rec), file=sys.stderr, flush=True)
-        del s
+        del band
         torch.cuda.empty_cache()
     print(json.dumps(out))
 

@@ -129,6 +129,10 @@ def main(root):
             if a and grbm:
                 d['valu_active_cycles_per_launch'] = 4.0 * a
                 d['valu_busy_frac'] = round(4.0 * a / (1024 * grbm / 8.0), 4)
+        wk = launches(os.path.join(root, shape + '_work'), prefix, f16, mm)
+        if wk:
+            # bench.py roofline.work: per launch, the same ISA (one library for all passes)
+            d['work_counters_per_launch'] = {c: mean(wk, c) for c in next(iter(wk.values()))[1]}
         f, w = mean(fe, 'FETCH_SIZE'), mean(wr, 'WRITE_SIZE')
         if f is not None and w is not None:
             d['fetch_kib'], d['write_kib'] = f, w

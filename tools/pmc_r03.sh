@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-3 PMC passes (rocprofv3, one --pmc run per pass, each under its own kill timeout) for
 # the roofline fields of bench.py: per launch SQ instruction / cycle counters + the clock,
-# FETCH_SIZE and WRITE_SIZE (separate passes: TCC slots), for
+# FETCH_SIZE and WRITE_SIZE (separate passes: TCC slots), for the level kernel a fourth pass of
+# its work counters (MFMA math ops, float64 instruction mix), for
 #   l12_c3   dm_corr_level12, C3 batch (64 tiles of S=128)          tools/kbench.py
 #   l12_c5   dm_corr_level12, C5 pair (256 tiles of S=256)          tools/kbench.py
 #   l12_c2   dm_corr_level12, C2 pair (64 tiles of S=64)            tools/kbench.py
@@ -20,6 +21,9 @@ OUT=$REPO/gpurun_out/pmc3_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+# the level kernel's work pass (round 6, bench.py roofline.work): i8 MFMA math ops / 512 and the
+# float64 VALU instruction mix (wave instructions), one pass of 7 SQ counters
+WORK="SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_INSTS_MFMA SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F32"
 for s in $SHAPES; do
   case $s in
     l12_c3) CMD="$REPO/tools/kbench.py --variants l12 --rounds 1 --tile 128 --grid 8" ;;
@@ -35,8 +39,10 @@ for s in $SHAPES; do
     v32mm_c3) CMD="$REPO/tools/vbench.py --mm --rounds 1 --tiles 64 --tile 128" ;;
     *) echo "unknown shape $s"; exit 2 ;;
   esac
-  for pass in sq fetch write; do
-    case $pass in sq) P="$SQ" ;; fetch) P="FETCH_SIZE" ;; write) P="WRITE_SIZE" ;; esac
+  PASSES="sq fetch write"
+  case $s in l12_*) PASSES="sq fetch write work" ;; esac
+  for pass in $PASSES; do
+    case $pass in sq) P="$SQ" ;; fetch) P="FETCH_SIZE" ;; write) P="WRITE_SIZE" ;; work) P="$WORK" ;; esac
     timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $P --output-format csv -d "$OUT/${s}_$pass" -o run -- \
         python3 $CMD > "$OUT/${s}_$pass.log" 2>&1
     echo "$s $pass done"
