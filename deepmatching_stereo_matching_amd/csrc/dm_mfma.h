@@ -195,6 +195,9 @@ __global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
 #ifndef DM_XCD_MAP
 #define DM_XCD_MAP 1
 #endif
+#ifndef DM_ABL_PAPPROX
+#define DM_ABL_PAPPROX 0   // ablation builds only (tools/abl_build.sh papprox, papprox2)
+#endif
 __device__ __forceinline__ int wg_logical()
 {
     const int b = blockIdx.x, n = gridDim.x;
@@ -970,7 +973,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
             double sum = 0.0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) { // ul, ur, ll, lr: left-to-right sum
+#if DM_ABL_PAPPROX
+                // ABLATION ONLY (tools/abl_build.sh papprox / papprox2; results WRONG): the price of
+                // pruning the child pows -- the bin-centre approximation (1/c_i)^y * 2^(yE) (two
+                // table reads and a multiply, within 0.21 % of pow14) for every child, and with
+                // DM_ABL_PAPPROX == 2 the exact pow for 2 of the lane's 8 children per row (4 per
+                // level-2 window row: one exact level-1 value per window, the ideal pruned count)
+                double pv;
+                if (DM_ABL_PAPPROX == 2 && m == 0 && r < 2) pv = pow14_zf(x[r], plds, mant);
+                else {
+                    const unsigned u = __float_as_uint(x[r]);
+                    const unsigned ofp = (u >> 10) & 0x1FF0u, og = (u >> 19) & 0xFF0u;
+                    pv = (*(const dm_d2 *)((const char *)plds.fp + ofp)).x * (*(const dm_d2 *)((const char *)plds.g32 + og)).x;
+                }
+#else
                 const double pv = pow14_zf(x[r], plds, mant);
+#endif
                 sum = r == 0 ? pv : sum + pv;
             }
             // level 1 = pow14(sum / 4), rectified where it is read: here when level 1 is

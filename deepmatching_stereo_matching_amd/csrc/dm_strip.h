@@ -27,6 +27,23 @@
 // the two kernels agree bit for bit.
 #pragma once
 
+// LDS hand-over inside one cell block: a workgroup barrier when the block spans NWc > 1 waves,
+// a wave barrier (with the LDS fences) when the block is one wave
+#ifndef DM_STRIP_WAVESYNC
+#define DM_STRIP_WAVESYNC 0   // 1: wave barriers for one-wave blocks (C2) -- A/B switch, measured neutral (round 6)
+#endif
+template <int NWc>
+__device__ __forceinline__ void block_sync()
+{
+    if constexpr (NWc > 1 || !DM_STRIP_WAVESYNC) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 template <int NWc, int NB, bool L2F, bool CL, int MINW>
 __global__ __launch_bounds__(64 * NWc * NB, MINW) void k_level12_strip(Geo g, Stats s, double *L1, double *L2,
                                                                        const dm_v4i *__restrict__ Bs,
@@ -160,7 +177,10 @@ __global__ __launch_bounds__(64 * NWc * NB, MINW) void k_level12_strip(Geo g, St
     }
     StripFrag f2;
     load_strip(f2, 0); // sweep 2's first row pair, in flight through the reduction
-    __syncthreads();
+    // the reduction's partial extremes: from the block's waves (a workgroup barrier), or with one
+    // wave per block (NWc == 1: C2) from this wave alone -- a wave barrier, so the workgroup's
+    // NB independent blocks do not wait for each other between the sweeps (round 6)
+    block_sync<NWc>();
     // per-patch normalisation constants {a_p, lo, hi, rmin, den, RN(1/den)} -> LDS (k_level1_mfq's)
     if (wc == 0 && (lane & 15) < 4) {
         const int r = lane & 15, grp = lane >> 4;
@@ -183,7 +203,7 @@ __global__ __launch_bounds__(64 * NWc * NB, MINW) void k_level12_strip(Geo g, St
         s.rmn[tb + p] = rmn;
         s.rmx[tb + p] = rmx;
     }
-    __syncthreads();
+    block_sync<NWc>();
 
     // ---- sweep 2: pool on y -> normalise + rectify -> children sum -> level 1 [-> level 2] ----
     const bool bflat = CL && __builtin_amdgcn_readfirstlane((int)(cell_flat(cst[sb][0][4]) || cell_flat(cst[sb][1][4]) ||

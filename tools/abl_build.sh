@@ -2,6 +2,12 @@
 # Ablation builds of the level kernel (timing upper bounds only; their results are WRONG):
 #   nobar   no barrier between the two waves of a workgroup in sweep 2 (dm_mfma.h:628)
 #   nopow   pow14_zf replaced by a widening multiply (the eight child pows per row pair)
+#   papprox  (round 6) the child pows replaced by the bin-centre approximation (1/c_i)^y 2^(yE):
+#           the floor of any pruning of the child pows (C3 k_level1_mfq only)
+#   papprox2 the same with 2 of a lane's 8 child pows per row exact: the ideal pruned count (one
+#           exact level-1 value per level-2 window), without the candidate bookkeeping
+#   ssync   (round 6) the strip kernel's one-wave cell blocks (C2) synchronised by workgroup
+#           barriers between the sweeps, as in round 5 (DM_STRIP_WAVESYNC=0; results exact)
 #   nosw1   sweep 1 (per-patch min / max) skipped
 #   pconst  pow14_zf's three LDS table reads at fixed rows (broadcast: no bank conflicts)
 #   pnoread pow14_zf without its LDS table reads (values from the index bits, no LDS)
@@ -53,6 +59,9 @@ s = s[:a] + '__device__ __forceinline__ double pow14_zf(float x, const PowLds &t
 open(p, 'w').write(s)
 PY
     ;;
+    papprox) EXTRA="-DDM_ABL_PAPPROX=1" ;;
+    ssync) EXTRA="-DDM_STRIP_WAVESYNC=0" ;;
+    papprox2) EXTRA="-DDM_ABL_PAPPROX=2" ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
     pconst) sed -i 's/    const unsigned ofp = (u >> 10) \& 0x1FF0u, og = (u >> 19) \& 0xFF0u;/    const unsigned ofp = (u \& 0u), og = (u \& 0u) + 16u;/' $d/csrc/dm_kernels.hip
             grep -q "ofp = (u & 0u)" $d/csrc/dm_kernels.hip || { echo "pconst patch failed"; exit 1; } ;;
