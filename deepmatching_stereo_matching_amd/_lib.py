@@ -20,7 +20,7 @@ HEADER = os.path.join(os.path.dirname(HERE), 'include', 'dmstereo.h')
 
 DM_OK, DM_ERR_ARG, DM_ERR_SHAPE, DM_ERR_UNSUPPORTED, DM_ERR_HIP = 0, -1, -2, -3, -4
 DM_VOLUME_F16, DM_VOLUME_MINMAX_KNOWN = 1, 2   # dm_corr_volume_ex flags
-DM_POW_F32, DM_POW_Q4, DM_POW_K, DM_POW_FULL = 0, 1, 2, 3   # dm_pow14_variant forms
+DM_POW_F32, DM_POW_Q4, DM_POW_K, DM_POW_FULL, DM_POW_Q4G, DM_POW_KG = 0, 1, 2, 3, 4, 5   # dm_pow14_variant forms
 DM_TM_CCOEFF, DM_TM_CCOEFF_NORMED = 4, 5
 METHODS = {'cv2.TM_CCOEFF_NORMED': DM_TM_CCOEFF_NORMED, 'cv2.TM_CCOEFF': DM_TM_CCOEFF}
 CAL_MODES = {'elevation': 0, 'elevation2': 1, 'distance': 2}

@@ -104,7 +104,8 @@ __device__ __forceinline__ double fma_sc(double a, double b, double c)
 }
 
 // dm_pow14_fast's arithmetic from r = fma(M, c_i, -1), table index i and 2^(yE) row G = {G, g}
-__device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const PowLds &t)
+template <typename T>
+__device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const T &t)
 {
     double q = fma_sc(r, DM_POWF_B5, DM_POWF_B4);
     q = fma_sc(q, r, DM_POWF_B3);
@@ -116,7 +117,8 @@ __device__ __forceinline__ double pow14_core_r(double r, int i, dm_d2 G, const P
     return fma(Pr.x, G.x, s);
 }
 
-__device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const PowLds &t)
+template <typename T>
+__device__ __forceinline__ double pow14_core(double M, int i, dm_d2 G, const T &t)
 {
     return pow14_core_r(fma(M, (double)t.fc32[i], -1.0), i, G, t);
 }
@@ -166,7 +168,8 @@ __device__ __forceinline__ unsigned mant_mask_vgpr()
     asm volatile("v_mov_b32 %0, 0x7fffff" : "=v"(m));
     return m;
 }
-__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)
+template <typename T>
+__device__ __forceinline__ double pow14_zf(float x, const T &t, unsigned mant = 0x7FFFFFu)
 {
     const unsigned u = __float_as_uint(x);
     // bitop3 truth table 0xEA = (src0 & src1) | src2
@@ -200,6 +203,73 @@ static_assert(DM_POWF_EMIN <= -297, "fast-path table must cover every level-1/le
 __device__ __forceinline__ double pow14_k(double x, const PowLds &t)
 {
     return pow14_zd(x, t) + (x - x); // 0 -> +0 (zero row), NaN -> NaN
+}
+
+// The float64 pows of the pruned level kernel (round 6, k_level12_prune in dm_prune.h) without
+// the gz rows: that kernel's level-1 x buffers need the LDS the 5 KB of gz took.  The 2^(yE) row
+// of a double whose exponent E is in [-126, 0] is g32[E + 127] -- the same {G, g} constants as
+// gz[E - EMIN + 1] -- so pow14_core gives the same bits; zero reads g32[0] = {0, 0} as gz[0]; NaN
+// (and the out-of-domain s / 4 > 1 of pow14_q4) the NaN row g32[255] as gz[DM_GZ_ROWS]; the rare
+// E < -126 takes dm_pow14_fast with the constant-memory tables (the same constants and
+// operations as pow14_core: fma(M, c_i, -1), the series, fma(Phi, G, fma(Phi, q, Plo) G)), or 0
+// below 2^EMIN where gz's clamp gives 0.  So pow14_q4g == pow14_q4 and pow14_kg == pow14_k bit
+// for bit on EVERY double (tests/test_pow_gpu.py through dm_pow14_variant).  T: any table
+// struct with fp, g32, fc32 (PowLds, PowLdsG).
+template <typename T>
+__device__ __forceinline__ double pow14_q4g(double s, const T &t)
+{
+    const uint64_t b = dm_bits_f64(s);
+    const unsigned hi = (unsigned)(b >> 32);
+    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int i = (int)((hi >> 11) & (DM_POWF_NT - 1));
+    const int be = (int)((hi >> 20) & 0x7FF);
+    int row = be - 898;                       // E(s / 4) + 127 = be - 1025 + 127
+    if (be != 0 && row < 1) [[unlikely]] {    // s / 4 < 2^-126 (and not 0)
+        if (be - 1025 < DM_POWF_EMIN) return 0.0;
+        return dm_pow14_fast(ldexp(s, -2), c_powf_c, c_powf_p, c_powf_g);
+    }
+    row = be == 0 ? 0 : (row > 127 ? 255 : row);
+    return pow14_core_r(fma(M, (double)t.fc32[i], -1.0), i, t.g32[row], t);
+}
+
+template <typename T>
+__device__ __forceinline__ double pow14_kg(double x, const T &t)
+{
+    const uint64_t b = dm_bits_f64(x);
+    const unsigned hi = (unsigned)(b >> 32);
+    const double M = dm_f64_bits((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int i = (int)((hi >> 11) & (DM_POWF_NT - 1));
+    const int be = (int)((hi >> 20) & 0x7FF);
+    int row = be - 896;                       // E + 127
+    if (be != 0 && row < 1) [[unlikely]] {    // x < 2^-126 (and not 0)
+        if (be - 1023 < DM_POWF_EMIN) return 0.0 + (x - x);
+        return dm_pow14_fast(x, c_powf_c, c_powf_p, c_powf_g) + (x - x);
+    }
+    row = be == 0 ? 0 : (row > 127 ? 127 : row);   // (pow14_zd's clamp: x > 1 reads the E = 0 row)
+    return pow14_core_r(fma(M, (double)t.fc32[i], -1.0), i, t.g32[row], t) + (x - x);
+}
+
+// the pow tables without gz (k_level12_prune): fp, g32 (rows 128..254 a hole the kernel uses for
+// its exchange arrays), fc32
+struct PowLdsG {
+    dm_d2 fp[DM_POWF_NT];
+    dm_d2 g32[256];
+    float fc32[DM_POWF_NT];
+};
+
+__device__ __forceinline__ void pow_lds_fill_g(PowLdsG &t, int tid, int nthreads)
+{
+    for (int i = tid; i < DM_POWF_NT; i += nthreads) {
+        t.fc32[i] = (float)c_powf_c[i];
+        t.fp[i] = dm_d2{c_powf_p[2 * i], c_powf_p[2 * i + 1]};
+    }
+    for (int b = tid; b < 256; b += nthreads) {
+        if (b >= 128 && b < 255) continue;
+        const int e = b - 127 - DM_POWF_EMIN;
+        const bool in = b >= 1 && b <= 127 && e >= 0;
+        t.g32[b] = in ? dm_d2{c_powf_g[2 * e], c_powf_g[2 * e + 1]}
+                   : b == 255 ? dm_d2{(double)NAN, (double)NAN} : dm_d2{0.0, 0.0};
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -359,6 +429,7 @@ __device__ double l1_value(const Geo &g, const Stats &s, int t, int I, int J, in
 
 #include "dm_mfma.h"
 #include "dm_strip.h"
+#include "dm_prune.h"
 
 // ------------------------------------------------------------------------------------
 // K2 (generic): one workgroup per level-1 cell (= 2x2 block of patches p).  For each
@@ -527,6 +598,8 @@ __global__ __launch_bounds__(256) void k_pow_variant(const double *in, size_t n,
         if constexpr (V == DM_POW_F32) r = pow14_zf((float)x, plds, mant);
         else if constexpr (V == DM_POW_Q4) r = pow14_q4(x, plds);
         else if constexpr (V == DM_POW_K) r = pow14_k(x, plds);
+        else if constexpr (V == DM_POW_Q4G) r = pow14_q4g(x, plds);
+        else if constexpr (V == DM_POW_KG) r = pow14_kg(x, plds);
         else r = pow14_lds(x, plds);
         out[i] = r;
     }
@@ -1472,6 +1545,21 @@ static int launch_level1(const dm_tiles *b, Stats s, double *L1, hipStream_t st)
 #ifndef DM_C2_NB
 #define DM_C2_NB 4   // one-wave cell blocks per workgroup of the S = 64 level kernel
 #endif
+// the C3 level kernel with pruned child pows when DM_PRUNE is set (dm_prune.h) -> launched?
+template <bool OK>
+static bool prune_c3(const Geo &gg, const Stats &s, double *L1, double *L2, const dm_v4i *Bw, const int2 *QS,
+                     const dm_v4i *Bs, const dm_v4i *Ss, unsigned grid, hipStream_t st)
+{
+    if constexpr (DM_PRUNE && OK) {
+        if (Bs && L1 == nullptr && L2 != nullptr) {
+            k_level12_prune<2, DM_C3_NB, DM_C3_MINW><<<grid, 64 * 2 * DM_C3_NB, 0, st>>>(gg, s, L2, Bw, QS, Bs, Ss);
+            return true;
+        }
+    }
+    (void)gg; (void)s; (void)L1; (void)L2; (void)Bw; (void)QS; (void)Bs; (void)Ss; (void)grid; (void)st;
+    return false;
+}
+
 template <bool L2F, bool YF>
 static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2 *QS, double *L1, double *L2,
                         hipStream_t st, const dm_v4i *Bs, const dm_v4i *Ss)
@@ -1514,6 +1602,9 @@ static int launch_mfq_t(const dm_tiles *b, Stats s, const dm_v4i *Bw, const int2
         const size_t bpt = (size_t)(b->h0 / 4) * (b->w0 / 4);
         if (bpt % NBc) return fail(DM_ERR_UNSUPPORTED, "cell blocks per tile not a multiple of %d (fill_ptab: a workgroup in one tile)", NBc);
         if (Bs && (DM_S2 & 2)) k_level12_strip<2, NBc, L2F, CL, DM_C3_MW><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, L1, L2, Bs, Ss);
+        // level 1 not stored: the child pows pruned to the level-2 window maxima (dm_prune.h;
+        // DM_PRUNE, off: measured slower)
+        else if (prune_c3<L2F && YF>(gg, s, L1, L2, Bw, QS, Bs, Ss, grid / NBc, st)) {}
         else if (Bs) k_level1_mfq<1, 4, 2 * NBc, DM_C3_MINW, L2F, YF, NBc, CL, YF><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2, Bs, Ss);
         else k_level1_mfq<1, 4, 2 * NBc, 4, L2F, YF, NBc, CL><<<grid / NBc, 64 * 2 * NBc, 0, st>>>(gg, s, Bw, QS, L1, L2);
         HIP_TRY(hipGetLastError());
@@ -1694,13 +1785,13 @@ static int launch_volume_mfq(const dm_tiles *b, void *d_stats, const Stats &s, O
 
 extern "C" {
 
-int dm_abi_version(void) { return 109; }
+int dm_abi_version(void) { return 110; }
 
 #define DM_STR2(x) #x
 #define DM_STR(x) DM_STR2(x)
 const char *dm_build_config(void)
 {
-    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " VS1=" DM_STR(DM_VS1) " VS1_LDS=" DM_STR(DM_VS1_LDS) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C3_MINW=" DM_STR(DM_C3_MINW) " C5_NB=" DM_STR(DM_C5_NB)
+    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " PRUNE=" DM_STR(DM_PRUNE) " VS1=" DM_STR(DM_VS1) " VS1_LDS=" DM_STR(DM_VS1_LDS) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C3_MINW=" DM_STR(DM_C3_MINW) " C5_NB=" DM_STR(DM_C5_NB)
            " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
            " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
            " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_HS_TR=" DM_STR(DM_VL_HS_TR) " VL_F_NW=" DM_STR(DM_VL_F_NW)
@@ -1885,6 +1976,8 @@ int dm_pow14_variant(int32_t variant, const double *d_in, size_t n, double *d_ou
     case DM_POW_F32: k_pow_variant<DM_POW_F32><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
     case DM_POW_Q4: k_pow_variant<DM_POW_Q4><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
     case DM_POW_K: k_pow_variant<DM_POW_K><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    case DM_POW_Q4G: k_pow_variant<DM_POW_Q4G><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
+    case DM_POW_KG: k_pow_variant<DM_POW_KG><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
     case DM_POW_FULL: k_pow_variant<DM_POW_FULL><<<grid, 256, 0, st>>>(d_in, n, d_out); break;
     default: return fail(DM_ERR_ARG, "unknown pow14 variant %d", variant);
     }

@@ -144,8 +144,11 @@ int dm_rectify64(const double *d_in, size_t n, double *d_out, void *stream);
  *                four children, level-1 / level-2 averaging); 0 < s / 4 < 2^-319 gives 0 and
  *                s = +inf NaN instead of dm_pow14's values
  *   DM_POW_K     pow14_k(x): 0, NaN and x in [2^-319, 1]
- *   DM_POW_FULL  pow14_lds(x): every double (the slow path outside [2^-319, 1]) */
-enum dm_pow_variant { DM_POW_F32 = 0, DM_POW_Q4 = 1, DM_POW_K = 2, DM_POW_FULL = 3 };
+ *   DM_POW_FULL  pow14_lds(x): every double (the slow path outside [2^-319, 1])
+ *   DM_POW_Q4G   pow14_q4g(s), DM_POW_KG pow14_kg(x) (ABI 1.10): the same as DM_POW_Q4 / DM_POW_K
+ *                bit for bit on EVERY double, from the float32-exponent table rows instead of
+ *                the float64 ones (the pruned level kernel, whose LDS holds no gz rows) */
+enum dm_pow_variant { DM_POW_F32 = 0, DM_POW_Q4 = 1, DM_POW_K = 2, DM_POW_FULL = 3, DM_POW_Q4G = 4, DM_POW_KG = 5 };
 int dm_pow14_variant(int32_t variant, const double *d_in, size_t n, double *d_out, void *stream);
 
 /* One pyramid step for levels >= 1: MaxPool2d(3,2,1) per map, (ul+ur+ll+lr)/4, and
@@ -285,13 +288,14 @@ const char *dm_build_config(void);
 /* Human-readable description of the last failure on this thread. */
 const char *dm_last_error(void);
 
-/* ABI version (major * 100 + minor): 109 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
+/* ABI version (major * 100 + minor): 110 (1.1 adds dm_corr_level12, 1.2 the fp16 volume
  * dm_corr_volume_f16 / dm_rectify_f16, 1.3 the Gauss-Seidel post-processing, 1.4 a larger
  * stats workspace: a second window-operand region for the volume kernels, window stats
  * carried inside the operand tiles, 1.5 dm_corr_volume_ex, 1.6 dm_pow14_variant and the
  * 4-tile column groups of dm_corr_stats' window operands at S = 128 / 256, 1.7 dm_seq_sum,
  * 1.8 dm_subpix_map, 1.9 dm_subpix_map_tiles and the row-pair strips of dm_corr_stats'
- * workspace for the level kernel's min / max sweep). */
+ * workspace for the level kernel's min / max sweep, 1.10 the DM_POW_Q4G / DM_POW_KG forms of
+ * dm_pow14_variant). */
 int dm_abi_version(void);
 
 #ifdef __cplusplus

@@ -24,7 +24,7 @@ def test_exports_every_header_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dm_abi_version() == 109
+    assert lib.dm_abi_version() == 110
 
 
 def test_stats_bytes(lib):

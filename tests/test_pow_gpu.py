@@ -107,3 +107,19 @@ def test_full_form_everywhere(lib):
     xs = np.concatenate([rng.random(20000), np.ldexp(rng.random(20000) + 1.0, rng.integers(-1074, 1023, 20000)),
                          [0.0, -0.0, 1.0, np.inf, -1.0, np.nan, 2.0 ** -1074, 2.0 ** -1022, 1.5, 1e300]])
     assert _same(_dev(lib, lib.DM_POW_FULL, xs), _host(xs))
+
+
+def test_g32_forms_equal_the_gz_forms_everywhere(lib):
+    """pow14_q4g / pow14_kg (the pruned level kernel's forms, no gz rows in LDS) equal pow14_q4 /
+    pow14_k bit for bit on every double: the domains, zero, NaN, +-inf, negatives, values above
+    1 and the rare inputs below 2^-126 (the constant-memory path) and below 2^-319 (0)."""
+    rng = np.random.default_rng(16)
+    xs = np.concatenate([rng.random(50000), 4.0 * rng.random(50000),
+                         np.ldexp(rng.random(40000) + 1.0, rng.integers(-1074, 1023, 40000)),
+                         np.ldexp(rng.random(20000) + 1.0, -rng.integers(120, 330, 20000)),
+                         4.0 * _bin_edges(-319, -1, rng, 512)[::5],
+                         [0.0, -0.0, 1.0, 4.0, np.inf, -np.inf, -1.0, np.nan, 2.0 ** -1074, 2.0 ** -1022,
+                          2.0 ** -126, 2.0 ** -127, 4.0 * 2.0 ** -126, 4.0 * 2.0 ** -127, 2.0 ** -319,
+                          2.0 ** -320, 4.0 * 2.0 ** -319, 4.0 * 2.0 ** -320, 1.5, 1e300]])
+    assert _same(_dev(lib, lib.DM_POW_Q4G, xs), _dev(lib, lib.DM_POW_Q4, xs))
+    assert _same(_dev(lib, lib.DM_POW_KG, xs), _dev(lib, lib.DM_POW_K, xs))

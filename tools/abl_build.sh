@@ -8,6 +8,8 @@
 #           exact level-1 value per level-2 window), without the candidate bookkeeping
 #   ssync   (round 6) the strip kernel's one-wave cell blocks (C2) synchronised by workgroup
 #           barriers between the sweeps, as in round 5 (DM_STRIP_WAVESYNC=0; results exact)
+#   prune0, prune1  (round 6) the C3 level kernel without / with the child-pow pruning
+#           (k_level1_mfq / k_level12_prune, DM_PRUNE; results exact)
 #   nosw1   sweep 1 (per-patch min / max) skipped
 #   pconst  pow14_zf's three LDS table reads at fixed rows (broadcast: no bank conflicts)
 #   pnoread pow14_zf without its LDS table reads (values from the index bits, no LDS)
@@ -53,14 +55,16 @@ for v in "$@"; do
     nopow) python3 - $d/csrc/dm_kernels.hip <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
-a = s.index('__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)\n{')
+a = s.index('__device__ __forceinline__ double pow14_zf(float x, const T &t, unsigned mant = 0x7FFFFFu)\n{')
 b = s.index('\n}\n', a)
-s = s[:a] + '__device__ __forceinline__ double pow14_zf(float x, const PowLds &t, unsigned mant = 0x7FFFFFu)\n{\n    return (double)x * 1.25;' + s[b:]
+s = s[:a] + '__device__ __forceinline__ double pow14_zf(float x, const T &t, unsigned mant = 0x7FFFFFu)\n{\n    return (double)x * 1.25;' + s[b:]
 open(p, 'w').write(s)
 PY
     ;;
     papprox) EXTRA="-DDM_ABL_PAPPROX=1" ;;
     ssync) EXTRA="-DDM_STRIP_WAVESYNC=0" ;;
+    prune0) EXTRA="-DDM_PRUNE=0" ;;
+    prune1) EXTRA="-DDM_PRUNE=1" ;;
     papprox2) EXTRA="-DDM_ABL_PAPPROX=2" ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
     pconst) sed -i 's/    const unsigned ofp = (u >> 10) \& 0x1FF0u, og = (u >> 19) \& 0xFF0u;/    const unsigned ofp = (u \& 0u), og = (u \& 0u) + 16u;/' $d/csrc/dm_kernels.hip
