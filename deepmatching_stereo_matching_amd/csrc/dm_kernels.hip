@@ -1791,7 +1791,7 @@ int dm_abi_version(void) { return 110; }
 #define DM_STR(x) DM_STR2(x)
 const char *dm_build_config(void)
 {
-    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " PRUNE=" DM_STR(DM_PRUNE) " VS1=" DM_STR(DM_VS1) " VS1_LDS=" DM_STR(DM_VS1_LDS) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C3_MINW=" DM_STR(DM_C3_MINW) " C5_NB=" DM_STR(DM_C5_NB)
+    return "S1=" DM_STR(DM_S1) " S2=" DM_STR(DM_S2) " PRUNE=" DM_STR(DM_PRUNE) " STRIP_WAVESYNC=" DM_STR(DM_STRIP_WAVESYNC) " VS1=" DM_STR(DM_VS1) " VS1_LDS=" DM_STR(DM_VS1_LDS) " XCD_MAP=" DM_STR(DM_XCD_MAP) " C2_NB=" DM_STR(DM_C2_NB) " C3_NB=" DM_STR(DM_C3_NB) " C3_MW=" DM_STR(DM_C3_MW) " C3_MINW=" DM_STR(DM_C3_MINW) " C5_NB=" DM_STR(DM_C5_NB)
            " VL_H_TR=" DM_STR(DM_VL_H_TR) " VL_H_NT=" DM_STR(DM_VL_H_NT) " VL_H_NW=" DM_STR(DM_VL_H_NW)
            " VL_H2_TR=" DM_STR(DM_VL_H2_TR) " VL_H2_NW=" DM_STR(DM_VL_H2_NW) " VL_F2_TR=" DM_STR(DM_VL_F2_TR)
            " VL_F2_MW=" DM_STR(DM_VL_F2_MW) " VL_HS_NW=" DM_STR(DM_VL_HS_NW) " VL_HS_TR=" DM_STR(DM_VL_HS_TR) " VL_F_NW=" DM_STR(DM_VL_F_NW)

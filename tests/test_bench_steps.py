@@ -26,6 +26,7 @@ import subprocess
 import sys
 
 import pytest
+import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -147,5 +148,19 @@ def test_rccl_world_one_gather_and_breakdown():
         bd = bench.split_breakdown(split, 0, 1, dev)
         assert len(bd) == 1 and bd[0]['rank'] == 0 and bd[0]['tiles'] == grid * grid
         assert bd[0]['compute_ms'] > 0 and bd[0]['gather_wait_ms'] >= 0 and bd[0]['chunks'] >= 1
+        # round 6: the product path through RCCL -- the pair sent by broadcast_pair, the mirror
+        # ImageCutSolver with tile sharding (shard.BandSolver, chunked gathers) -- equals the
+        # bench's split solve (the same BandSolver) and the unsharded mirror
+        from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
+        p1, p2 = shard.broadcast_pair(a, b, src=0, device=dev)
+        assert p1.is_cuda and torch.equal(p1.cpu(), torch.from_numpy(a)) and torch.equal(p2.cpu(), torch.from_numpy(b))
+        plain = ImageCutSolver(a, b, image_size=[S, S], stride=[S, S], window_size=WS)()
+        with shard.tile_sharding():
+            assert not shard.tile_sharding_enabled()      # one rank: the mirror solves it whole
+        d_band, o_band = shard.solve_image_sharded(a, b, [S, S], [S, S], WS, 5, ('elevation',), sub_pix=True,
+                                                   filtering_mode='median', result='all', chunks=2)
+        assert np.array_equal(d_band.cpu().numpy(), plain[0], equal_nan=True)
+        assert np.array_equal(o_band.cpu().numpy(), plain[1], equal_nan=True)
+        assert torch.equal(bench._bits(d_band), bench._bits(r_whole[0]))
     finally:
         tdist.destroy_process_group()

@@ -2,9 +2,11 @@
 of the test box, gloo process group (RCCL refuses two ranks on one device; the per-tile
 results are gathered through host copies, shard._gather_units).
 
-Every rank runs shard.solve_image_sharded -> engine.solve_tiles (its tiles r::N) ->
-_gather_units -> engine.stitch, and the mirror ImageCutSolver()() with the process group
-initialised (it dispatches to shard).  Both must equal a single-process solve byte for
+Every rank receives the pair from rank 0 (shard.broadcast_pair) and runs
+shard.solve_image_sharded -> shard.BandSolver (its contiguous band of tiles, chunk by chunk,
+each chunk gathered to rank 0) -> engine.stitch on rank 0 -> the maps broadcast, and the mirror
+ImageCutSolver()() with the process group initialised (it dispatches to shard; with
+tile_sharding(result='root') only rank 0 gets the maps).  Both must equal a single-process solve byte for
 byte, and the oracle's ImageCutSolver (misc/image_cut_solver.py:144-179) bit for bit.
 """
 import os
@@ -34,12 +36,19 @@ def _worker(rank, size, port, q):
         torch.cuda.set_device(0)
         from deepmatching_stereo_matching_amd import shard
         from deepmatching_stereo_matching_amd.misc.image_cut_solver import ImageCutSolver
-        a, b = _case()
+        a, b = _case() if rank == 0 else (None, None)
+        a, b = (t.cpu().numpy() for t in shard.broadcast_pair(a, b, src=0))   # only rank 0 has the pair
         d, s = shard.solve_image_sharded(a, b, [S, S], STRIDE, WS, 5, MODES)
         cut = ImageCutSolver(a, b, image_size=[S, S], stride=STRIDE, window_size=WS,
                              degree_map_mode=list(MODES))
         with shard.tile_sharding():      # opt-in: every rank solves this same pair together
             d2, s2 = cut()
+        with shard.tile_sharding(result='root'):   # the maps on rank 0 only (no broadcast)
+            d3, s3 = ImageCutSolver(a, b, image_size=[S, S], stride=STRIDE, window_size=WS,
+                                    degree_map_mode=list(MODES))()
+        assert (d3 is None and s3 is None) == (rank != 0)
+        if rank == 0:
+            assert np.array_equal(d3, d2, equal_nan=True) and np.array_equal(s3, s2, equal_nan=True)
         dist.barrier()
         q.put((rank, d.cpu().numpy(), s.cpu().numpy(), d2, s2))
     except BaseException as e:   # report, do not hang the parent

@@ -29,7 +29,7 @@ VOLUME = ((128, 4, False), (128, 4, True), (128, 2, False), (128, 2, True),
 # DEFAULTS mirror the C defaults of dm_kernels.hip (every key dm_build_config reports); they
 # only fill keys a library's config string lacks -- a library that cannot be loaded at all is
 # an error (symbol() raises), never a guess.
-DEFAULTS = {'S1': 1, 'S2': 5, 'VS1': 1, 'VS1_LDS': 1, 'XCD_MAP': 1, 'C2_NB': 4, 'C3_NB': 2, 'C3_MW': 4,
+DEFAULTS = {'S1': 1, 'S2': 5, 'PRUNE': 0, 'STRIP_WAVESYNC': 0, 'VS1': 1, 'VS1_LDS': 1, 'XCD_MAP': 1, 'C2_NB': 4, 'C3_NB': 2, 'C3_MW': 4,
             'C3_MINW': 4, 'C5_NB': 1, 'VL_H_TR': 2, 'VL_H_NT': 1, 'VL_H_NW': 4,
             'VL_H2_TR': 0, 'VL_H2_NW': 8, 'VL_F2_TR': 0, 'VL_F2_MW': 1, 'VL_HS_NW': 8, 'VL_HS_TR': 0,
             'VL_F_NW': 8, 'VL_F_TR': 4, 'VL_F_MW': 4, 'VL_F_NT': 1}
@@ -81,6 +81,8 @@ def symbol(kind, tile, esz=None, mm=False, lib=None):
         nwc = 1 if tile == 64 else 2 if tile == 128 else 4
         if (c['S2'] >> {64: 0, 128: 1, 256: 2}[tile]) & 1:   # both sweeps on the strips (dm_strip.h)
             return 'k_level12_stripILi%dELi%dELb1ELb1ELi%dEE' % (nwc, nb, c['C3_MW'] if tile == 128 else 4)
+        if tile == 128 and c['PRUNE']:   # round 6: the pruned C3 kernel (dm_prune.h), when built in
+            return 'k_level12_pruneILi2ELi%dELi%dEE' % (nb, c['C3_MINW'])
         minw = c['C3_MINW'] if tile == 128 else 4
         return 'k_level1_mfqILi1ELi4ELi%dELi%dELb1ELb1ELi%dELb1ELb%dEE' % (nb * nwc, minw, nb, c['S1'])
     if (tile, esz, bool(mm)) not in VOLUME:
