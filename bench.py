@@ -681,8 +681,9 @@ def check_step_outputs(held, solvers, dist, steps):
 def c5_split(args, rank, world, dev, dist):
     """BASELINE configs[4] / north_star's "tiled 4096^2 pairs" line: one 4096^2 pair (16 x 16
     tiles of S = 256, the reference's ImageCutSolver loop, image_cut_solver.py:144-179) per
-    step with its 256 tiles split over the ranks (rank r solves tiles r::N) and gathered to
-    rank 0 (RCCL over xGMI), which stitches.  Timed like the main line (warmup, barrier +
+    step with its 256 tiles split over the ranks (shard.BandSolver: rank r solves one
+    contiguous band of tiles in chunks, each chunk gathered to rank 0 over RCCL / xGMI behind
+    the compute), and rank 0 stitches.  Timed like the main line (warmup, barrier +
     synchronize, max over ranks), outputs checked like it.  With N > 1, rank 0 then solves the
     whole pair alone on its GPU (the other ranks wait at a barrier): the N = 1 reference of
     the same run, so speedup = its ms_per_pair / the split's."""
