@@ -43,6 +43,8 @@
 #   c3nb1, c3nb4   the S = 128 level kernel with 1 / 4 two-wave cell blocks per workgroup instead of 2
 #   c5nb2   the S = 256 level kernel with 2 four-wave cell blocks per workgroup instead of 1
 #           (DM_C3_NB / DM_C5_NB; results exact)
+#   nofill  (round 6) the strip kernel (C2 / C5) without its pow-table fill: the price of the
+#           workgroup prologue's table copy (results wrong)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -66,6 +68,8 @@ PY
     prune0) EXTRA="-DDM_PRUNE=0" ;;
     prune1) EXTRA="-DDM_PRUNE=1" ;;
     papprox2) EXTRA="-DDM_ABL_PAPPROX=2" ;;
+    nofill) sed -i 's/^    pow_lds_fill(plds, tid, 64 \* NW, false);$/    (void)plds;/' $d/csrc/dm_strip.h
+            grep -q "^    (void)plds;" $d/csrc/dm_strip.h || { echo "nofill patch failed"; exit 1; } ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
     pconst) sed -i 's/    const unsigned ofp = (u >> 10) \& 0x1FF0u, og = (u >> 19) \& 0xFF0u;/    const unsigned ofp = (u \& 0u), og = (u \& 0u) + 16u;/' $d/csrc/dm_kernels.hip
             grep -q "ofp = (u & 0u)" $d/csrc/dm_kernels.hip || { echo "pconst patch failed"; exit 1; } ;;
