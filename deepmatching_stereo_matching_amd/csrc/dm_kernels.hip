@@ -1798,6 +1798,17 @@ const char *dm_build_config(void)
            " VL_F_TR=" DM_STR(DM_VL_F_TR) " VL_F_MW=" DM_STR(DM_VL_F_MW) " VL_F_NT=" DM_STR(DM_VL_F_NT);
 }
 
+#if DM_CLOCK_STAMP
+// diagnostic builds only (DM_CLOCK_STAMP, dm_mfma.h): the level kernels' per-workgroup clock
+// stamps of the last launch, {shader start, shader end, real start, real end} per workgroup
+int dm_diag_clock_stamps(unsigned long long *host, int nwg)
+{
+    if (nwg < 0 || nwg > 65536) return fail(DM_ERR_ARG, "nwg %d outside 0 .. 65536", nwg);
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(dm_clock_stamps), (size_t)nwg * 4 * sizeof(unsigned long long)));
+    return DM_OK;
+}
+#endif
+
 const char *dm_last_error(void) { return g_err; }
 
 size_t dm_stats_bytes(const dm_tiles *b)

@@ -198,6 +198,33 @@ __global__ void k_prep_strips(Geo g, dm_v4i *Bs, dm_v4i *Ss)
 #ifndef DM_ABL_PAPPROX
 #define DM_ABL_PAPPROX 0   // ablation builds only (tools/abl_build.sh papprox, papprox2)
 #endif
+// In-kernel clock of the level kernels (diagnostic builds only: tools/abl_build.sh clk,
+// MI355X_MICROARCH.md 'DVFS give-back' item 6): wave 0 of every workgroup reads the shader
+// clock counter and the 100 MHz real-time counter when the workgroup starts and when it
+// ends, and writes the four values (vector stores) to dm_clock_stamps, which no other code
+// reads; dm_diag_clock_stamps copies them out.  Clock = d(shader) / d(real) x 100 MHz.
+#ifndef DM_CLOCK_STAMP
+#define DM_CLOCK_STAMP 0
+#endif
+#if DM_CLOCK_STAMP
+__device__ unsigned long long dm_clock_stamps[4 * 65536];
+struct ClockStamp {
+    long long t0, r0;
+    __device__ ClockStamp() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~ClockStamp()
+    {
+        const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            unsigned long long *p = dm_clock_stamps + 4 * (blockIdx.x & 65535u);
+            p[0] = (unsigned long long)t0; p[1] = (unsigned long long)t1;
+            p[2] = (unsigned long long)r0; p[3] = (unsigned long long)r1;
+        }
+    }
+};
+#define DM_CLOCK_STAMP_HERE ClockStamp dm_clock_stamp_;
+#else
+#define DM_CLOCK_STAMP_HERE
+#endif
 __device__ __forceinline__ int wg_logical()
 {
     const int b = blockIdx.x, n = gridDim.x;
@@ -524,6 +551,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_level1_mfq(Geo g, Stats s, co
                                                         const dm_v4i *__restrict__ Bs = nullptr,
                                                         const dm_v4i *__restrict__ Ss = nullptr)
 {
+    DM_CLOCK_STAMP_HERE
     constexpr bool EQ = KS == 1 && YF;           // window stats ride in the B tile (qs_of_frag)
     static_assert(NW % NB == 0, "blocks split the waves evenly");
     static_assert(!CL || L2F, "clamp-bit normalisation: NaN cells are restored at the level-2 / level-1 stores");

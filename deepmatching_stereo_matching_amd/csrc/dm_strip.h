@@ -49,6 +49,7 @@ __global__ __launch_bounds__(64 * NWc * NB, MINW) void k_level12_strip(Geo g, St
                                                                        const dm_v4i *__restrict__ Bs,
                                                                        const dm_v4i *__restrict__ Ss)
 {
+    DM_CLOCK_STAMP_HERE
     constexpr int NW = NWc * NB;
     constexpr bool RICH = MINW < 4;   // register budget of 3 waves / SIMD (or fewer)
     static_assert(!CL || L2F, "clamp-bit normalisation: NaN cells are restored at the level-2 / level-1 stores");

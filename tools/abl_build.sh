@@ -45,6 +45,8 @@
 #           (DM_C3_NB / DM_C5_NB; results exact)
 #   nofill  (round 6) the strip kernel (C2 / C5) without its pow-table fill: the price of the
 #           workgroup prologue's table copy (results wrong)
+#   clk     (round 6) the level kernels with per-workgroup clock stamps (DM_CLOCK_STAMP=1;
+#           results exact, tools/clock_probe.py reads them)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
 # travels to the GPU box); tools/ab3.sh / kbench A/B them with DM_LIB_PATH.
 set -euo pipefail
@@ -68,6 +70,7 @@ PY
     prune0) EXTRA="-DDM_PRUNE=0" ;;
     prune1) EXTRA="-DDM_PRUNE=1" ;;
     papprox2) EXTRA="-DDM_ABL_PAPPROX=2" ;;
+    clk) EXTRA="-DDM_CLOCK_STAMP=1" ;;
     nofill) sed -i 's/^    pow_lds_fill(plds, tid, 64 \* NW, false);$/    (void)plds;/' $d/csrc/dm_strip.h
             grep -q "^    (void)plds;" $d/csrc/dm_strip.h || { echo "nofill patch failed"; exit 1; } ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
