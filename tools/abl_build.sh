@@ -45,6 +45,10 @@
 #           (DM_C3_NB / DM_C5_NB; results exact)
 #   nofill  (round 6) the strip kernel (C2 / C5) without its pow-table fill: the price of the
 #           workgroup prologue's table copy (results wrong)
+#   bwrow0, strow0  (round 6) C3 k_level1_mfq with every sweep-2 window-operand load (bwrow0) or
+#           every sweep-1 strip load (strow0) at row 0: the same instructions, served from the
+#           CU's vector cache instead of L2 (row index masked by a run-time zero, so the loads stay in
+#           the loop) -- the price of the L2 read traffic (results wrong)
 #   clk     (round 6) the level kernels with per-workgroup clock stamps (DM_CLOCK_STAMP=1;
 #           results exact, tools/clock_probe.py reads them)
 # Each is the in-tree source with one sed patch, built to ab/libdm_<name>.so (git-ignored,
@@ -71,6 +75,10 @@ PY
     prune1) EXTRA="-DDM_PRUNE=1" ;;
     papprox2) EXTRA="-DDM_ABL_PAPPROX=2" ;;
     clk) EXTRA="-DDM_CLOCK_STAMP=1" ;;
+    bwrow0) sed -i 's/^            const unsigned ti = (unsigned)q0 \* G + tw;$/            const unsigned ti = (unsigned)(q0 \& (g.h0 >> 16)) * G + tw;/' $d/csrc/dm_mfma.h
+            grep -q "(unsigned)(q0 & (g.h0 >> 16)) \* G + tw;" $d/csrc/dm_mfma.h || { echo "bwrow0 patch failed"; exit 1; } ;;
+    strow0) sed -i 's/^                f.b\[j\] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)(rp \* NT32 + j) \* 1024u, 0);$/                f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rS1, voS, (unsigned)((rp \& (g.h0 >> 16)) * NT32 + j) * 1024u, 0);/' $d/csrc/dm_mfma.h
+            grep -q "(unsigned)((rp & (g.h0 >> 16)) \* NT32 + j) \* 1024u" $d/csrc/dm_mfma.h || { echo "strow0 patch failed"; exit 1; } ;;
     nofill) sed -i 's/^    pow_lds_fill(plds, tid, 64 \* NW, false);$/    (void)plds;/' $d/csrc/dm_strip.h
             grep -q "^    (void)plds;" $d/csrc/dm_strip.h || { echo "nofill patch failed"; exit 1; } ;;
     nosw1) sed -i '457s/q0 < h0; q0 += 2) {/q0 < 0; q0 += 2) {/' $d/csrc/dm_mfma.h ;;
